@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X closed-loop hot path (BASELINE.json metric:
+env-steps/s at 65,536 parallel episodes per GPU; mean tracking error vs the
+reference).
+
+Workload (BASELINE.json configs[1]): per GPU 65,536
+independent 30 s episodes (3,000 steps at dt = 0.01), linear target,
+Riccati-LQR with the default weights (one shared DARE gain), seeds = global
+episode index.  One bench "step" = one full pass of the hot path over the
+batch: reset kernel (inputs already in HBM) -> fused closed-loop rollout
+kernel (3,000 steps of compute_action -> env.step with fused metric
+accumulation) -> per-episode metrics kernel -> summary partials (+ one RCCL
+all-reduce of the metric vector when N > 1).  value = all ranks' env-steps /
+max-over-ranks wall time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+(N > 1 is launched by torch.distributed.run, one process per GPU.)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lqr-quadcopter-test_amd"))
+
+# Algorithmic FP64 operations per episode-step of the config-2 loop (LQR,
+# linear target, RK4), counted from the reference arithmetic with each sin,
+# cos, sqrt and fmod as one operation (DESIGN.md §4 has the table):
+# controller 58 + Evaluator metric accumulation 22 + env.step 349.
+FLOPS_PER_ENV_STEP = 429
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, spec (half the FP32 vector 157.3 TF/s)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--episodes", type=int, default=65536, help="episodes per GPU")
+    ap.add_argument("--motion", default="linear")
+    ap.add_argument("--cpu-sample", type=int, default=8192, help="episodes in the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.env.config import EnvConfig
+    from quadtrack.rollout import build_batch, max_steps_for
+
+    n = args.episodes
+    cfg = EnvConfig.from_dict({"target": {"motion_type": args.motion}})
+    env = cfg.to_params()
+    crit = core.criteria()
+
+    # ---- setup (untimed): gains, seeded reset draws uploaded to HBM
+    t_dare0 = time.perf_counter()
+    ctl = BatchedRiccatiLQR({"dt": 0.01}, device=dev)
+    torch.cuda.synchronize()
+    t_dare = time.perf_counter() - t_dare0
+    lo = rank * n
+    seeds = lo + np.arange(n)
+    batch = build_batch(ctl, cfg, n, seeds=seeds)
+    st = core.RolloutState.empty(n, dev)
+    core.validate(batch, st)
+    nsteps = max_steps_for(env)
+
+    stream = torch.cuda.current_stream(dev)
+    ev = []
+
+    def one_pass(timed: bool):
+        core.reset(env, batch, st)
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        core.rollout(env, ctl.ctrl, crit, batch, st, nsteps)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        met = core.episode_metrics(crit, st)
+        part = core.summary_partials(met)
+        if world > 1:
+            dist.all_reduce(part[0:5])  # RCCL over xGMI: the one data exchange
+        return met
+
+    for _ in range(args.warmup):
+        one_pass(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        met = one_pass(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    steps_done = met[core._abi.MET["steps"]].sum()
+    local_env_steps = float(steps_done.item())  # this rank's executed env-steps per pass
+    if world > 1:
+        dist.all_reduce(steps_done)
+    env_steps_per_pass = float(steps_done.item())  # all ranks, executed steps of the last pass
+    value = env_steps_per_pass * args.steps / elapsed
+
+    res_summary = None
+    from quadtrack.parallel import summary_from_partials
+    from quadtrack.utils.metrics import SuccessCriteria
+
+    res_summary = summary_from_partials(met, SuccessCriteria(), global_offset=lo)
+
+    # ---- DARE throughput (per-episode gains, config-4 style), reported beside
+    dare = None
+    if rank == 0:
+        rng = np.random.default_rng(42)
+        m = n
+        qp = rng.uniform([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0], (m, 3))
+        qv = rng.uniform([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0], (m, 3))
+        rc = rng.uniform(0.5, 2.0, (m, 4))
+        BatchedRiccatiLQR({"dt": 0.01}, device=dev, q_pos=qp[:256], q_vel=qv[:256], r_controls=rc[:256])
+        torch.cuda.synchronize()
+        td = time.perf_counter()
+        b = BatchedRiccatiLQR({"dt": 0.01}, device=dev, q_pos=qp, q_vel=qv, r_controls=rc)
+        torch.cuda.synchronize()
+        td = time.perf_counter() - td
+        dare = {"problems": m, "seconds_incl_host_setup": round(td, 4), "solves_per_s": round(m / td, 1),
+                "max_iterations": int(b.iters.max().item()), "shared_gain_solve_s": round(t_dare, 4)}
+
+    cpu = None
+    track = {"mean_tracking_error": res_summary.mean_tracking_error,
+             "mean_on_target_ratio": res_summary.mean_on_target_ratio}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, diff = cpu_baseline(args, cfg, seeds[: args.cpu_sample], met[:, : args.cpu_sample])
+        track["oracle_sample_episodes"] = int(min(args.cpu_sample, n))
+        track["oracle_sample_max_abs_diff"] = diff
+
+    if rank == 0:
+        achieved = FLOPS_PER_ENV_STEP * local_env_steps / (kern_ms * 1e-3) / 1e12
+        line = {
+            "metric": "env-steps/sec at 65 536 parallel episodes per GPU (30 s @ dt=0.01, Riccati-LQR closed loop)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: seeded reset draws (numpy default_rng per episode, as the reference), "
+                    "seeds = global episode index",
+            "config": {"workload": f"BASELINE configs[1]: {n} episodes/GPU x {nsteps - 2} steps, {args.motion} "
+                                   f"target, Riccati-LQR shared K, RK4 dt=0.01",
+                       "episodes_per_gpu": n, "episodes_total": n * world, "parallelism": f"episode-sharded x{world}"},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "rollout_kernel<LINEAR,6,false>", "kernel_ms": round(kern_ms, 4),
+                         "flops_per_env_step": FLOPS_PER_ENV_STEP},
+            "cpu_baseline": cpu,
+            "tracking": track,
+            "dare": dare,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg, seeds, gpu_met):
+    """The oracle (C restatement of the reference loop, oracle/) on the host
+    cores over a bounded sample of the same episodes; also returns the max
+    |GPU - oracle| over that sample's per-episode metrics."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    env = O.env_params({"target": {"motion_type": args.motion}})
+    c, K, kc, _, _ = O.controller({"dt": 0.01})
+    pat, off = O.draws(args.motion, seeds)
+    x0 = np.array([O.initial_state(env, env.motion, pat[i], off[i]) for i in range(len(seeds))])
+    t0 = time.perf_counter()
+    met, xf, _, threads = O.rollout(env, c, O.criteria(), None, pat, None, None, K, kc, False, x0,
+                                    threads=args.cpu_threads or None)
+    dt = time.perf_counter() - t0
+    steps = float(met[:, -1].sum())
+    diff = float(np.max(np.abs(gpu_met.cpu().numpy().T - met)))
+    cpu = {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": int(threads), "kind": "port",
+           "sample": f"{len(seeds)} episodes x 3000 steps of the same workload (oracle/qt_oracle.c, FP64, "
+                     f"OpenMP over episodes), {dt:.2f} s wall",
+           "cpu_model": _cpu_model()}
+    return cpu, diff
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

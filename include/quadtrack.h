@@ -1,0 +1,253 @@
+/*
+ * quadtrack.h — C ABI of the MI355X batched quadcopter-tracking hot path.
+ *
+ * This is the drop-in boundary for the reference's closed-loop
+ * `RiccatiLQRController.compute_action` -> `QuadcopterEnv.step` loop
+ * (AgentFoundryExamples/lqr-quadcopter-test, src/quadcopter_tracking/...).
+ * Every entry point takes plain pointers and sizes; every array pointer is a
+ * DEVICE pointer (HBM, e.g. the data_ptr() of a torch tensor on cuda:N) and
+ * every call is asynchronous on the given HIP stream (`stream` is a
+ * hipStream_t passed as void*; NULL = the legacy default stream).
+ * The library keeps no global state.  Return value: 0 on success, a negative
+ * QT_E* code on an invalid argument or a HIP launch error.
+ *
+ * Layout conventions (HBM, FP64, structure-of-arrays):
+ *   state  x[12][n]   rows: px py pz vx vy vz roll pitch yaw p q r
+ *                     (quadcopter_env.py:63-70)
+ *   aux    integ[3][n] LQI integral state (riccati_lqr.py:484-486)
+ *   time   t[n]       per-episode accumulated time (t += dt, quadcopter_env.py:191)
+ *   gains  K[kcols*4][m] SoA: element (row r, col c) of episode e at
+ *                     K[(r*kcols + c)*m + e], with m = n (per-episode gains)
+ *                     or m = 1 (one shared gain matrix, k_per_episode = 0).
+ */
+#ifndef QUADTRACK_H
+#define QUADTRACK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QT_ABI_VERSION 1
+
+/* error codes */
+#define QT_OK 0
+#define QT_EINVAL (-1)
+#define QT_ELAUNCH (-2)
+
+/* TargetMotion.VALID_MOTION_TYPES (target_motion.py:264-270) */
+enum qt_motion {
+  QT_MOTION_STATIONARY = 0,
+  QT_MOTION_LINEAR = 1,
+  QT_MOTION_CIRCULAR = 2,
+  QT_MOTION_SINUSOIDAL = 3,
+  QT_MOTION_FIGURE8 = 4
+};
+
+/* QuadcopterEnv._check_termination reasons (quadcopter_env.py:513-535) */
+enum qt_term {
+  QT_TERM_RUNNING = 0,
+  QT_TERM_TIME_LIMIT = 1,
+  QT_TERM_POSITION_BOUNDS = 2,
+  QT_TERM_NUMERICAL_INSTABILITY = 3
+};
+
+/* solve_dare outcome per episode (riccati_lqr.py:153-178) */
+enum qt_dare_status {
+  QT_DARE_OK = 0,
+  QT_DARE_Q_NOT_PSD = 1,      /* "Q matrix must be positive semi-definite" */
+  QT_DARE_R_NOT_PD = 2,       /* "R matrix must be positive definite" */
+  QT_DARE_NO_CONVERGE = 3,    /* "DARE solver failed" */
+  QT_DARE_SINGULAR = 4        /* singular (R + B'PB) / doubling matrix */
+};
+
+/* Plant + target + success parameters: EnvConfig (env/config.py:11-95). */
+typedef struct qt_env_params {
+  /* QuadcopterParams (config.py:12-38); Ixx/Iyy/Izz/arm_length/k_* are never
+     read by the dynamics and are not carried. */
+  double mass, gravity, drag_linear, drag_angular;
+  double min_thrust, max_thrust, max_angular_rate;
+  /* SimulationParams (config.py:41-51) */
+  double dt, max_episode_time, max_velocity, max_angular_velocity, max_position;
+  int32_t integrator;   /* 0 = "rk4", 1 = "euler" (quadcopter_env.py:309-312) */
+  int32_t motion;       /* enum qt_motion, used when no per-episode motion array */
+  /* TargetParams (config.py:55-65) */
+  double speed, amplitude, frequency, radius, center[3], max_acceleration;
+  /* SuccessCriteria of the ENV (config.py:69-74): post-step on-target and
+     info["success"] (quadcopter_env.py:204-226, 537-553) */
+  double target_radius, min_on_target_ratio, min_episode_duration;
+} qt_env_params;
+
+/* RiccatiLQRController options that shape compute_action
+   (riccati_lqr.py:418-535, 779-967). */
+typedef struct qt_ctrl_params {
+  double dt;                                 /* integral step */
+  double hover_thrust;                       /* mass * gravity (riccati_lqr.py:471) */
+  double min_thrust, max_thrust, max_rate;   /* output clamps (907-921) */
+  int32_t use_lqi;                           /* K has 9 columns when set */
+  int32_t feedforward_enabled;
+  double integral_limit, integral_zero_threshold;
+  double ff_velocity_gain[3], ff_acceleration_gain[3];
+  double ff_max_velocity, ff_max_acceleration;
+} qt_ctrl_params;
+
+/* Evaluator criteria for the per-episode metrics (utils/metrics.py:26-39);
+   these are the Evaluator's own, distinct from qt_env_params' criteria. */
+typedef struct qt_criteria {
+  double min_on_target_ratio, min_episode_duration, target_radius;
+  int32_t overshoot_window;                  /* detect_overshoots window_size */
+  int32_t pad_;
+} qt_criteria;
+
+/* Per-episode running accumulators kept in HBM between rollout chunks.
+   Row index into acc[QT_ACC_ROWS][n] (doubles). */
+enum qt_acc_row {
+  QT_ACC_SUM_ERR = 0,      /* sum of pre-step tracking errors (metrics.py:300) */
+  QT_ACC_SUM_ERR2,         /* sum of squares (rms, metrics.py:330) */
+  QT_ACC_MAX_ERR,          /* max pre-step error (NaN-propagating like np.max) */
+  QT_ACC_ON_PRE,           /* count err_pre <= criteria.target_radius */
+  QT_ACC_ON_POST,          /* env post-step on-target count (quadcopter_env.py:205-207) */
+  QT_ACC_SUM_EFFORT,       /* sum |u|_2 (metrics.py:182-202) */
+  QT_ACC_OS_COUNT,         /* overshoot count (metrics.py:205-261) */
+  QT_ACC_OS_MAX,           /* max overshoot */
+  QT_ACC_OS_CUR,           /* overshoot state machine: current phase max */
+  QT_ACC_OS_STREAK,        /* off-target streak (-1 = not in an overshoot phase) */
+  QT_ACC_PREV_ON,          /* on-target flag of the previous pre-step error (-1 = none) */
+  QT_ACC_STEPS,            /* executed steps */
+  QT_ACC_VIOLATIONS,       /* steps with an action violation (quadcopter_env.py:174-181) */
+  QT_ACC_TERM,             /* enum qt_term */
+  QT_ACC_ROWS
+};
+
+/* Final per-episode metrics, row index into met[QT_MET_ROWS][n] (doubles),
+   EpisodeMetrics field order (utils/metrics.py:42-73). */
+enum qt_met_row {
+  QT_MET_DURATION = 0, QT_MET_ON_TARGET_RATIO, QT_MET_MEAN_ERR, QT_MET_MAX_ERR,
+  QT_MET_RMS_ERR, QT_MET_TOTAL_EFFORT, QT_MET_MEAN_EFFORT, QT_MET_OS_COUNT,
+  QT_MET_OS_MAX, QT_MET_SUCCESS, QT_MET_TERM, QT_MET_VIOLATIONS,
+  QT_MET_ENV_ON_TARGET_RATIO, QT_MET_STEPS, QT_MET_ROWS
+};
+
+/* Per-episode inputs of a batch.  NULL optional arrays fall back to the
+   scalar in the params structs.  `order` (optional) maps work slot -> episode
+   so that a launch can walk episodes grouped by motion type. */
+typedef struct qt_batch {
+  int64_t n;                    /* episodes */
+  const int8_t* motion;         /* [n] enum qt_motion, or NULL */
+  const double* pattern;        /* [4][n]: linear raw normal draw xyz (normalised twice in
+                                   kernel, target_motion.py:320-321,47) | circular theta0 |
+                                   sinusoidal phase xyz (target_motion.py:306-369) */
+  const double* plant_mass;     /* [n] or NULL -> env.mass */
+  const double* hover_thrust;   /* [n] or NULL -> ctrl.hover_thrust */
+  const double* K;              /* gains, layout above */
+  int32_t k_cols;               /* 6 (LQR) or 9 (LQI) */
+  int32_t k_per_episode;        /* 0: one shared K (m = 1), 1: m = n */
+  const int32_t* order;         /* [n] or NULL */
+} qt_batch;
+
+/* Mutable per-episode rollout state, all [.][n] SoA device arrays. */
+typedef struct qt_state {
+  double* x;          /* [12][n] */
+  double* integ;      /* [3][n]  LQI integral (may be NULL when !use_lqi) */
+  double* t;          /* [n] */
+  double* acc;        /* [QT_ACC_ROWS][n] */
+  double* target;     /* [9][n] target p,v,a at t (the observation the controller sees next) */
+} qt_state;
+
+/* ---------------------------------------------------------------- entry points */
+
+/* ABI version of the loaded library. */
+int qt_abi_version(void);
+
+/* QuadcopterEnv.reset(seed) from pre-drawn randoms (quadcopter_env.py:111-150):
+   x = [p_target(0) + offset, 0...], t = 0, accumulators cleared, target row
+   filled with the t = 0 observation, LQI integral zeroed (fresh controller,
+   riccati_lqr.py:1073-1086).  offset[3][n] = uniform(-0.5, 0.5, 3) draws. */
+int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset,
+             qt_state st, void* stream);
+
+/* The fused closed loop: `nsteps` iterations of
+   compute_action (riccati_lqr.py:779-967) -> env.step (quadcopter_env.py:152-232)
+   per episode, register-resident, with the Evaluator's per-episode metric
+   accumulation fused (eval.py:119-159, utils/metrics.py:264-338).  Episodes that
+   are done stay frozen.  May be called repeatedly (chunks).  If rec != NULL it
+   receives, for every step s of this call, x after the step at
+   rec[((s*16 + j) * n) + e] for j < 12 and the applied controller action at j = 12..15. */
+int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+               const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, void* stream);
+
+/* Open-loop QuadcopterEnv.step(action) for a batch (quadcopter_env.py:152-293):
+   action[4][n] (NaN/Inf zeroed, thrust and rate clipping), RK4/Euler, state
+   constraints, t += dt, post-step error and termination.  Outputs:
+   err[n] (info["tracking_error"]), on_target[n] (0/1), done[n] (0/1),
+   term[n] (enum qt_term), violation[n] (0/1 for this step).  Counters in
+   acc (ON_POST, STEPS, VIOLATIONS, TERM) are updated.  Episodes already done are
+   stepped anyway (the reference does not refuse a step after done). */
+int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action,
+                qt_state st, double* err, int8_t* on_target, int8_t* done, int8_t* term,
+                int8_t* violation, void* stream);
+
+/* RiccatiLQRController.compute_action for a batch of observations
+   (riccati_lqr.py:779-967).  obs[15][n]: quad pos(3), quad vel(3), target
+   pos(3), target vel(3), target acc(3).  integ[3][n] is updated in LQI mode.
+   action[4][n] out; saturated[n] (0/1) out (may be NULL); diag[16][n] (may be
+   NULL) receives get_control_components() (969-978): state_error(6),
+   feedback_u(4), ff_velocity_term(3), ff_acceleration_term(3). */
+int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs,
+                      double* integ, double* action, int8_t* saturated, double* diag, void* stream);
+
+/* TargetMotion.get_state(t) (target_motion.py:387-411) for every episode at
+   per-episode times t[n]: out[9][n] = position, velocity, clamped acceleration. */
+int qt_target_state(const qt_env_params* env, const qt_batch* batch, const double* t,
+                    double* out, void* stream);
+
+/* Finalise accumulators into EpisodeMetrics rows (utils/metrics.py:264-338). */
+int qt_episode_metrics(const qt_criteria* crit, int64_t n, const double* acc, const double* t,
+                       double* met, void* stream);
+
+/* compute_episode_metrics over recorded per-step arrays (utils/metrics.py:144-338):
+   qpos/tpos [steps][3][n], actions [steps][4][n], last_time[n]; steps[n] valid
+   rows per episode.  Writes met[QT_MET_ROWS][n] (TERM/VIOLATIONS rows are 0). */
+int qt_metrics_from_arrays(const qt_criteria* crit, int64_t n, int32_t max_steps,
+                           const double* qpos, const double* tpos, const double* actions,
+                           const int32_t* steps, const double* last_time, double* met,
+                           void* stream);
+
+/* Batched DARE + gain (solve_dare, riccati_lqr.py:119-184) for the linearised
+   hover model (build_linearized_system / build_augmented_lqi_system,
+   riccati_lqr.py:187-316) with per-episode mass and cost matrices.
+   n_state = 6 (LQR) or 9 (LQI).  q[n_state*n_state][m], r[16][m]: full matrices,
+   SoA per element (row-major element index), m = number of problems.
+   Validation follows _is_positive_semidefinite / _is_positive_definite
+   (riccati_lqr.py:57-116).  Outputs: K[4*n_state][m] (SoA), P[n_state^2][m]
+   (may be NULL), status[m] (enum qt_dare_status), iters[m] (may be NULL).
+   structured != 0 asserts Q, R are diagonal (the per-axis decoupled fast
+   path: one lane per (problem, axis)); 0 runs the dense one-wavefront solver. */
+int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gravity,
+                    const double* mass, const double* q, const double* r,
+                    int32_t structured, double* K, double* P, int8_t* status,
+                    int32_t* iters, void* stream);
+
+/* General dense DARE + gain (solve_dare, riccati_lqr.py:119-184) for arbitrary
+   systems: n <= 16 states, p <= 8 inputs, m problems.  A[n*n][m'] and B[n*p][m']
+   SoA with m' = m (ab_per_problem = 1) or 1 (shared); q[n*n][m], r[p*p][m].
+   Outputs K[p*n][m], P[n*n][m] (may be NULL), status[m], iters[m] (may be NULL).
+   No heuristic fallback: failed problems get K = 0 and a nonzero status. */
+int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, const double* B,
+                  int32_t ab_per_problem, const double* q, const double* r, double* K, double* P,
+                  int8_t* status, int32_t* iters, void* stream);
+
+/* EvaluationSummary reductions (utils/metrics.py:341-390) over met[QT_MET_ROWS][n],
+   one workgroup, fixed order (bitwise reproducible).  out[11] (device):
+   [sum ratio, sum mean_err, sum mean_effort, sum success, count,
+    sum (ratio - mu_ratio)^2, sum (mean_err - mu_err)^2,
+    max ratio, first argmax, min ratio, first argmin].  A second call with the
+   means of the first gives the population std (np.std) without cancellation. */
+int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QUADTRACK_H */

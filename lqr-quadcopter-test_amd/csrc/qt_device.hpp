@@ -1,0 +1,388 @@
+// qt_device.hpp — per-episode device math of the closed loop, FP64.
+//
+// Everything here is a register-resident restatement of one episode's
+// arithmetic; the kernels in qt_rollout.hip map one episode to one lane and
+// keep state, target, gains and accumulators in VGPRs (shared gains in
+// SGPRs) across thousands of steps.  Reference functions are cited as
+// file:line relative to src/quadcopter_tracking/ of the reference repo.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/quadtrack.h"
+
+namespace qt {
+
+constexpr double kPi = 3.141592653589793;
+constexpr double kTwoPi = 6.283185307179586;  // 2 * np.pi
+constexpr double kMaxTilt = kPi / 3.0;        // math.pi / 3 (quadcopter_env.py:461)
+
+// np.clip == minimum(maximum(v, lo), hi): NaN propagates (a NaN action is
+// zeroed later by the env, quadcopter_env.py:266-269).
+__device__ __forceinline__ double clipd(double v, double lo, double hi) {
+  double r = v < lo ? lo : v;
+  return r > hi ? hi : r;
+}
+
+__device__ __forceinline__ double norm3(double a, double b, double c) { return sqrt(a * a + b * b + c * c); }
+
+// numpy float remainder: floor-mod, sign of the divisor (quadcopter_env.py:457)
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+// np.sign equality used by the LQI anti-windup (riccati_lqr.py:881-883):
+// sign(NaN) is NaN, which equals nothing.
+__device__ __forceinline__ bool same_sign(double a, double b) {
+  if (a != a || b != b) return false;
+  int sa = (a > 0) - (a < 0), sb = (b > 0) - (b < 0);
+  return sa == sb;
+}
+
+// ---------------------------------------------------------------- target
+
+// Per-episode constants of a motion pattern, precomputed once per launch.
+struct Pattern {
+  double c0, c1, c2;  // linear: velocity xyz | circular: theta0, omega | sinusoidal: phases
+  double o0, o1, o2;  // sinusoidal: omegas | figure8: omega
+};
+
+// TargetMotion._create_pattern + pattern constructors (target_motion.py:306-369,
+// 32-49, 62-82, 121-140, 156-172): raw draw -> per-episode constants.
+__device__ __forceinline__ Pattern make_pattern(const qt_env_params& e, int motion, double r0, double r1,
+                                                double r2) {
+  Pattern p{0, 0, 0, 0, 0, 0};
+  if (motion == QT_MOTION_LINEAR) {
+    // direction /= norm (321), then direction / norm(direction) (47), * speed (49)
+    double n1 = norm3(r0, r1, r2);
+    double d0 = r0 / n1, d1 = r1 / n1, d2 = r2 / n1;
+    double n2 = norm3(d0, d1, d2);
+    p.c0 = (d0 / n2) * e.speed;
+    p.c1 = (d1 / n2) * e.speed;
+    p.c2 = (d2 / n2) * e.speed;
+  } else if (motion == QT_MOTION_CIRCULAR) {
+    p.c0 = r0;
+    p.c1 = e.speed / e.radius;
+  } else if (motion == QT_MOTION_SINUSOIDAL) {
+    p.c0 = r0;
+    p.c1 = r1;
+    p.c2 = r2;
+    p.o0 = 2.0 * kPi * e.frequency;
+    p.o1 = 2.0 * kPi * (e.frequency * 1.3);
+    p.o2 = 2.0 * kPi * (e.frequency * 0.7);
+  } else if (motion == QT_MOTION_FIGURE8) {
+    p.o0 = e.speed / e.amplitude;
+  }
+  return p;
+}
+
+struct Target {
+  double p[3], v[3], a[3];
+};
+
+// pattern.get_state(t) (target_motion.py:51-248) + TargetMotion.get_state's
+// acceleration clamp (403-405).  WANT_ACC = false skips the acceleration,
+// which only the feed-forward path reads (riccati_lqr.py:853-861).
+template <bool WANT_ACC>
+__device__ __forceinline__ void target_state(const qt_env_params& e, int motion, const Pattern& pt, double t,
+                                             Target& o) {
+  o.p[0] = e.center[0];
+  o.p[1] = e.center[1];
+  o.p[2] = e.center[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o.v[i] = 0.0, o.a[i] = 0.0;
+  if (motion == QT_MOTION_LINEAR) {
+    o.p[0] = e.center[0] + pt.c0 * t;
+    o.p[1] = e.center[1] + pt.c1 * t;
+    o.p[2] = e.center[2] + pt.c2 * t;
+    o.v[0] = pt.c0;
+    o.v[1] = pt.c1;
+    o.v[2] = pt.c2;
+  } else if (motion == QT_MOTION_CIRCULAR) {
+    double ang = pt.c0 + pt.c1 * t;
+    double s, c;
+    sincos(ang, &s, &c);
+    const double r = e.radius, om = pt.c1;
+    o.p[0] = e.center[0] + r * c;
+    o.p[1] = e.center[1] + r * s;
+    o.v[0] = -r * om * s;
+    o.v[1] = r * om * c;
+    if (WANT_ACC) {
+      o.a[0] = -r * (om * om) * c;
+      o.a[1] = -r * (om * om) * s;
+    }
+  } else if (motion == QT_MOTION_SINUSOIDAL) {
+    const double amp[3] = {e.amplitude, e.amplitude * 0.5, e.amplitude * 0.25};
+    const double om[3] = {pt.o0, pt.o1, pt.o2};
+    const double ph[3] = {pt.c0, pt.c1, pt.c2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double s, c;
+      sincos(om[i] * t + ph[i], &s, &c);
+      o.p[i] = e.center[i] + amp[i] * s;
+      o.v[i] = amp[i] * om[i] * c;
+      if (WANT_ACC) o.a[i] = -amp[i] * (om[i] * om[i]) * s;
+    }
+  } else if (motion == QT_MOTION_FIGURE8) {
+    const double sc = e.amplitude, om = pt.o0;
+    double st, ct;
+    sincos(om * t, &st, &ct);
+    double den = 1.0 + st * st;
+    o.p[0] = e.center[0] + sc * ct / den;
+    o.p[1] = e.center[1] + sc * st * ct / den;
+    double dcos = -st * om, dsin = ct * om;
+    double dden = 2.0 * st * dsin;
+    double den2 = den * den;
+    o.v[0] = sc * ((dcos * den - ct * dden) / den2);
+    o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
+    if (WANT_ACC) {
+      // the reference's 1e-6 forward difference (target_motion.py:215-229)
+      const double h = 1e-6;
+      double stp, ctp;
+      sincos(om * (t + h), &stp, &ctp);
+      double denp = 1.0 + stp * stp;
+      double pp0 = e.center[0] + sc * ctp / denp;
+      double pp1 = e.center[1] + sc * stp * ctp / denp;
+      o.a[0] = ((pp0 - o.p[0]) / h - o.v[0]) / h;
+      o.a[1] = ((pp1 - o.p[1]) / h - o.v[1]) / h;
+      o.a[2] = 0.0;
+    }
+  }
+  if (WANT_ACC) {
+    double am = norm3(o.a[0], o.a[1], o.a[2]);
+    if (am > e.max_acceleration) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) o.a[i] = o.a[i] / am * e.max_acceleration;
+    }
+  }
+}
+
+// ----------------------------------------------------------------- plant
+
+// Per-lane plant constants: 1/mass and the gravity force (quadcopter_env.py:396).
+struct Plant {
+  double inv_mass, gz;
+};
+
+__device__ __forceinline__ Plant make_plant(const qt_env_params& e, double mass) {
+  return Plant{1.0 / mass, -mass * e.gravity};
+}
+
+// _compute_derivatives (quadcopter_env.py:329-426).  Only the third column of
+// the ZYX rotation matrix multiplies the body thrust [0,0,T] (393).  Divisions
+// by mass and by the 0.1 s rate time constant are taken as multiplications by
+// reciprocals (<= 1 ulp per term; the closed loop is not chaotic).
+__device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant& pl, const double* s,
+                                            const double* u, double* d) {
+  double sphi, cphi, sth, cth, spsi, cpsi;
+  sincos(s[6], &sphi, &cphi);
+  sincos(s[7], &sth, &cth);
+  sincos(s[8], &spsi, &cpsi);
+  const double T = u[0];
+  const double tw0 = (cpsi * sth * cphi + spsi * sphi) * T;
+  const double tw1 = (spsi * sth * cphi - cpsi * sphi) * T;
+  const double tw2 = (cth * cphi) * T;
+  d[0] = s[3];
+  d[1] = s[4];
+  d[2] = s[5];
+  d[3] = (tw0 + (-e.drag_linear * s[3])) * pl.inv_mass;
+  d[4] = (tw1 + (-e.drag_linear * s[4])) * pl.inv_mass;
+  d[5] = ((tw2 + pl.gz) + (-e.drag_linear * s[5])) * pl.inv_mass;
+  d[6] = s[9];
+  d[7] = s[10];
+  d[8] = s[11];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[9 + i] = (u[1 + i] - s[9 + i]) * 10.0 - e.drag_angular * s[9 + i];
+}
+
+// _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held
+// constant across the four stages.
+__device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
+  const double dt = e.dt;
+  double k[12];
+  derivatives(e, pl, x, u, k);
+  if (e.integrator == 1) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
+    return;
+  }
+  double acc[12], tmp[12];
+  const double h2 = 0.5 * dt;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    acc[i] = k[i];
+    tmp[i] = x[i] + h2 * k[i];
+  }
+  derivatives(e, pl, tmp, u, k);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    acc[i] = acc[i] + 2.0 * k[i];
+    tmp[i] = x[i] + h2 * k[i];
+  }
+  derivatives(e, pl, tmp, u, k);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    acc[i] = acc[i] + 2.0 * k[i];
+    tmp[i] = x[i] + dt * k[i];
+  }
+  derivatives(e, pl, tmp, u, k);
+  const double h6 = dt / 6.0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = x[i] + h6 * (acc[i] + k[i]);
+}
+
+// _apply_state_constraints (quadcopter_env.py:428-465)
+__device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
+  double vm = norm3(x[3], x[4], x[5]);
+  if (vm > e.max_velocity) {
+#pragma unroll
+    for (int i = 3; i < 6; ++i) x[i] = x[i] / vm * e.max_velocity;
+  }
+#pragma unroll
+  for (int i = 9; i < 12; ++i) x[i] = clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+#pragma unroll
+  for (int i = 6; i < 9; ++i) x[i] = py_mod(x[i] + kPi, kTwoPi) - kPi;
+  x[6] = clipd(x[6], -kMaxTilt, kMaxTilt);
+  x[7] = clipd(x[7], -kMaxTilt, kMaxTilt);
+}
+
+// _parse_and_validate_action (quadcopter_env.py:234-293) on an array action;
+// returns true when any violation was recorded.
+__device__ __forceinline__ bool parse_action(const qt_env_params& e, const double* in, double* a) {
+  bool viol = false;
+  bool finite = isfinite(in[0]) && isfinite(in[1]) && isfinite(in[2]) && isfinite(in[3]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = (finite || isfinite(in[i])) ? in[i] : 0.0;
+  viol = !finite;
+  if (a[0] < e.min_thrust) {
+    viol = true;
+    a[0] = e.min_thrust;
+  } else if (a[0] > e.max_thrust) {
+    viol = true;
+    a[0] = e.max_thrust;
+  }
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    if (fabs(a[i]) > e.max_angular_rate) {
+      viol = true;
+      a[i] = clipd(a[i], -e.max_angular_rate, e.max_angular_rate);
+    }
+  }
+  return viol;
+}
+
+// _check_termination (quadcopter_env.py:513-535)
+__device__ __forceinline__ int termination(const qt_env_params& e, double t, const double* x) {
+  if (t >= e.max_episode_time) return QT_TERM_TIME_LIMIT;
+  if (fabs(x[0]) > e.max_position || fabs(x[1]) > e.max_position || fabs(x[2]) > e.max_position)
+    return QT_TERM_POSITION_BOUNDS;
+  bool fin = true;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) fin = fin && isfinite(x[i]);
+  return fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY;
+}
+
+// ------------------------------------------------------------ controller
+
+// Gains as seen by one lane: 4 x KC, loaded once per launch.
+template <int KC>
+struct Gains {
+  double k[4 * KC];
+};
+
+// RiccatiLQRController.compute_action (riccati_lqr.py:779-967) given the
+// observation the env returned (quad p, v; target p, v, a).  LQI integral
+// update 869-900, output clamps 907-921.  Returns true when saturated.
+template <int KC, bool FF>
+__device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC>& G, double hover,
+                                               const double* qp, const double* qv, const Target& tg,
+                                               double* integ, double* u, double* diag = nullptr) {
+  double ep[3], ev[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ep[i] = tg.p[i] - qp[i];
+  if (FF && c.feedforward_enabled) {
+    double vm = norm3(tv[0], tv[1], tv[2]);
+    if (vm > c.ff_max_velocity) {
+      double scl = c.ff_max_velocity / vm;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) tv[i] = tv[i] * scl;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      ffv[i] = c.ff_velocity_gain[i] * tv[i];  // diagnostics term (riccati_lqr.py:851)
+      tv[i] = (1.0 + c.ff_velocity_gain[i]) * tv[i];
+    }
+    double ac[3] = {tg.a[0], tg.a[1], tg.a[2]};
+    double am = norm3(ac[0], ac[1], ac[2]);
+    if (am > c.ff_max_acceleration && am > 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ac[i] = ac[i] / am * c.ff_max_acceleration;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ffa[i] = c.ff_acceleration_gain[i] * ac[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ev[i] = tv[i] - qv[i];
+  const double s[6] = {ep[0], ep[1], ep[2], ev[0], ev[1], ev[2]};
+  double uf[4];
+  if (KC == 9) {
+    double em = norm3(ep[0], ep[1], ep[2]);
+    const double lim = c.integral_limit;
+    if (em > c.integral_zero_threshold) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bool sat = fabs(integ[i]) >= lim && lim > 0;
+        bool worse = same_sign(integ[i], ep[i]);
+        if (!(sat && worse)) integ[i] += c.dt * ep[i];
+      }
+    }
+    if (lim > 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i], -lim, lim);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) a += G.k[r * KC + j] * s[j];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) b += G.k[r * KC + 6 + j] * integ[j];
+      uf[r] = a + b;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) a += G.k[r * KC + j] * s[j];
+      uf[r] = a;
+    }
+  }
+  const double raw0 = hover + uf[0] + ffa[2];
+  const double raw1 = uf[1] + -ffa[1];
+  const double raw2 = uf[2] + ffa[0];
+  const double raw3 = uf[3];
+  u[0] = clipd(raw0, c.min_thrust, c.max_thrust);
+  u[1] = clipd(raw1, -c.max_rate, c.max_rate);
+  u[2] = clipd(raw2, -c.max_rate, c.max_rate);
+  u[3] = clipd(raw3, -c.max_rate, c.max_rate);
+  if (diag) {  // get_control_components (riccati_lqr.py:946-954)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) diag[i] = s[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) diag[6 + i] = uf[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) diag[10 + i] = ffv[i], diag[13 + i] = ffa[i];
+  }
+  return (u[0] != raw0) || (u[1] != raw1) || (u[2] != raw2) || (u[3] != raw3);
+}
+
+}  // namespace qt

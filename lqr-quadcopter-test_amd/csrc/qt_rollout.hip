@@ -1,0 +1,638 @@
+// qt_rollout.hip — batched closed-loop kernels and their C ABI (include/quadtrack.h).
+//
+// One lane = one episode.  A launch walks `nsteps` closed-loop steps with the
+// whole episode (12-state plant, target pattern constants, 4x6 / 4x9 gains,
+// LQI integral, metric accumulators) resident in registers; HBM is touched
+// only to load the state at the start of a chunk and to store it at the end.
+// Reference functions: src/quadcopter_tracking/... of the reference repo.
+#include <hip/hip_runtime.h>
+
+#include "qt_device.hpp"
+
+using namespace qt;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Acc {
+  double sum_e, sum_e2, max_e, sum_u, os_max, os_cur;
+  int on_pre, on_post, os_count, os_streak, prev_on, steps, viol, term;
+};
+
+__device__ __forceinline__ Acc load_acc(const double* acc, int64_t n, int64_t e) {
+  Acc a;
+  a.sum_e = acc[QT_ACC_SUM_ERR * n + e];
+  a.sum_e2 = acc[QT_ACC_SUM_ERR2 * n + e];
+  a.max_e = acc[QT_ACC_MAX_ERR * n + e];
+  a.on_pre = (int)acc[QT_ACC_ON_PRE * n + e];
+  a.on_post = (int)acc[QT_ACC_ON_POST * n + e];
+  a.sum_u = acc[QT_ACC_SUM_EFFORT * n + e];
+  a.os_count = (int)acc[QT_ACC_OS_COUNT * n + e];
+  a.os_max = acc[QT_ACC_OS_MAX * n + e];
+  a.os_cur = acc[QT_ACC_OS_CUR * n + e];
+  a.os_streak = (int)acc[QT_ACC_OS_STREAK * n + e];
+  a.prev_on = (int)acc[QT_ACC_PREV_ON * n + e];
+  a.steps = (int)acc[QT_ACC_STEPS * n + e];
+  a.viol = (int)acc[QT_ACC_VIOLATIONS * n + e];
+  a.term = (int)acc[QT_ACC_TERM * n + e];
+  return a;
+}
+
+__device__ __forceinline__ void store_acc(double* acc, int64_t n, int64_t e, const Acc& a) {
+  acc[QT_ACC_SUM_ERR * n + e] = a.sum_e;
+  acc[QT_ACC_SUM_ERR2 * n + e] = a.sum_e2;
+  acc[QT_ACC_MAX_ERR * n + e] = a.max_e;
+  acc[QT_ACC_ON_PRE * n + e] = a.on_pre;
+  acc[QT_ACC_ON_POST * n + e] = a.on_post;
+  acc[QT_ACC_SUM_EFFORT * n + e] = a.sum_u;
+  acc[QT_ACC_OS_COUNT * n + e] = a.os_count;
+  acc[QT_ACC_OS_MAX * n + e] = a.os_max;
+  acc[QT_ACC_OS_CUR * n + e] = a.os_cur;
+  acc[QT_ACC_OS_STREAK * n + e] = a.os_streak;
+  acc[QT_ACC_PREV_ON * n + e] = a.prev_on;
+  acc[QT_ACC_STEPS * n + e] = a.steps;
+  acc[QT_ACC_VIOLATIONS * n + e] = a.viol;
+  acc[QT_ACC_TERM * n + e] = a.term;
+}
+
+struct BatchDev {
+  int64_t n;
+  const int8_t* motion;
+  const double* pattern;
+  const double* plant_mass;
+  const double* hover;
+  const double* K;
+  int32_t k_per_episode;
+  const int32_t* order;
+};
+
+__device__ __forceinline__ int64_t episode_of(const BatchDev& b, int64_t slot) {
+  return b.order ? (int64_t)b.order[slot] : slot;
+}
+
+__device__ __forceinline__ int motion_of(const BatchDev& b, const qt_env_params& e, int64_t ep) {
+  return b.motion ? (int)b.motion[ep] : e.motion;
+}
+
+__device__ __forceinline__ Pattern pattern_of(const BatchDev& b, const qt_env_params& e, int motion, int64_t ep) {
+  const int64_t n = b.n;
+  double r0 = 0, r1 = 0, r2 = 0;
+  if (b.pattern) {
+    r0 = b.pattern[0 * n + ep];
+    r1 = b.pattern[1 * n + ep];
+    r2 = b.pattern[2 * n + ep];
+  }
+  return make_pattern(e, motion, r0, r1, r2);
+}
+
+template <int KC>
+__device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<KC>& G) {
+  if (b.k_per_episode) {
+#pragma unroll
+    for (int j = 0; j < 4 * KC; ++j) G.k[j] = b.K[(int64_t)j * b.n + ep];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4 * KC; ++j) G.k[j] = b.K[j];  // uniform address: scalar loads
+  }
+}
+
+// Overshoot state machine of detect_overshoots (utils/metrics.py:205-261),
+// streamed over the pre-step errors: called for every step k >= 1 with the
+// on-target flag of step k (the flag of k-1 is a.prev_on).  os_streak is the
+// off-target streak while in an overshoot phase, -1 outside one.
+__device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int window) {
+  const bool prev = a.prev_on > 0;
+  const bool in_phase = a.os_streak >= 0;
+  if (prev && !on) {
+    a.os_streak = 1;
+    a.os_cur = over;
+  } else if (in_phase && !on) {
+    a.os_streak += 1;
+    if (over > a.os_cur) a.os_cur = over;
+  } else if (in_phase && on) {
+    if (a.os_streak >= window) {
+      a.os_count += 1;
+      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
+    }
+    a.os_streak = -1;
+    a.os_cur = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------ reset
+
+__global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev b, const double* __restrict__ off,
+                                                       qt_state st) {
+  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.n) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  const int motion = motion_of(b, e, ep);
+  const Pattern pt = pattern_of(b, e, motion, ep);
+  Target tg;
+  target_state<true>(e, motion, pt, 0.0, tg);  // quadcopter_env.py:133-139
+#pragma unroll
+  for (int i = 0; i < 3; ++i) st.x[i * n + ep] = tg.p[i] + off[i * n + ep];
+#pragma unroll
+  for (int i = 3; i < 12; ++i) st.x[i * n + ep] = 0.0;
+  if (st.integ) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) st.integ[i * n + ep] = 0.0;
+  }
+  st.t[ep] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st.target[i * n + ep] = tg.p[i];
+    st.target[(3 + i) * n + ep] = tg.v[i];
+    st.target[(6 + i) * n + ep] = tg.a[i];
+  }
+  Acc a{0, 0, -INFINITY, 0, 0, 0, 0, 0, 0, -1, -1, 0, 0, QT_TERM_RUNNING};
+  store_acc(st.acc, n, ep, a);
+}
+
+// ---------------------------------------------------------------- rollout
+
+// MOTION >= 0 specialises the target pattern; -1 reads it per episode.
+template <int MOTION, int KC, bool FF>
+__global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+                                                         BatchDev b, qt_state st, int nsteps,
+                                                         double* __restrict__ rec) {
+  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.n) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
+  const Pattern pt = pattern_of(b, e, motion, ep);
+  const Plant pl = make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
+  const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
+  Gains<KC> G;
+  load_gains<KC>(b, ep, G);
+
+  double x[12], integ[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
+  if (KC == 9) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) integ[i] = st.integ[i * n + ep];
+  }
+  Target tg;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    tg.p[i] = st.target[i * n + ep];
+    tg.v[i] = st.target[(3 + i) * n + ep];
+    tg.a[i] = st.target[(6 + i) * n + ep];
+  }
+  double t = st.t[ep];
+  Acc a = load_acc(st.acc, n, ep);
+  const double R = cr.target_radius;
+
+  for (int s = 0; s < nsteps; ++s) {
+    if (a.term != QT_TERM_RUNNING) break;
+    // ---- compute_action on the current observation (riccati_lqr.py:779-967)
+    double u[4];
+    compute_action<KC, FF>(c, G, hover, x, x + 3, tg, integ, u);
+    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
+    const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+    const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+    a.sum_e += err;
+    a.sum_e2 += err * err;
+    if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
+    const bool on = err <= R;
+    a.on_pre += on;
+    a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+    if (a.prev_on >= 0) {
+      overshoot_step(a, on, err - R, cr.overshoot_window);
+    }
+    a.prev_on = on;
+    // ---- env.step (quadcopter_env.py:152-232)
+    double ua[4];
+    a.viol += parse_action(e, u, ua);
+    integrate(e, pl, x, ua);
+    constrain(e, x);
+    t += e.dt;
+    target_state<FF>(e, motion, pt, t, tg);
+    const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+    a.on_post += sqrt(q0 * q0 + q1 * q1 + q2 * q2) <= e.target_radius;
+    a.term = termination(e, t, x);
+    a.steps += 1;
+    if (rec) {
+      double* r = rec + (int64_t)s * 16 * n + ep;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) r[i * n] = x[i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[(12 + i) * n] = u[i];
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
+  if (KC == 9) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) st.integ[i * n + ep] = integ[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st.target[i * n + ep] = tg.p[i];
+    st.target[(3 + i) * n + ep] = tg.v[i];
+    st.target[(6 + i) * n + ep] = tg.a[i];
+  }
+  st.t[ep] = t;
+  store_acc(st.acc, n, ep, a);
+}
+
+// ------------------------------------------------------ open-loop env.step
+
+__global__ __launch_bounds__(kBlock) void env_step_kernel(qt_env_params e, BatchDev b,
+                                                          const double* __restrict__ action, qt_state st,
+                                                          double* err_out, int8_t* on_out, int8_t* done_out,
+                                                          int8_t* term_out, int8_t* viol_out) {
+  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.n) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  const int motion = motion_of(b, e, ep);
+  const Pattern pt = pattern_of(b, e, motion, ep);
+  const Plant pl = make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
+  double x[12], u[4], ua[4];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = action[i * n + ep];
+  const bool viol = parse_action(e, u, ua);
+  integrate(e, pl, x, ua);
+  constrain(e, x);
+  double t = st.t[ep] + e.dt;
+  Target tg;
+  target_state<true>(e, motion, pt, t, tg);
+  const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+  const double err = sqrt(q0 * q0 + q1 * q1 + q2 * q2);
+  const bool on = err <= e.target_radius;
+  const int term = termination(e, t, x);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st.target[i * n + ep] = tg.p[i];
+    st.target[(3 + i) * n + ep] = tg.v[i];
+    st.target[(6 + i) * n + ep] = tg.a[i];
+  }
+  st.t[ep] = t;
+  st.acc[QT_ACC_ON_POST * n + ep] += on;
+  st.acc[QT_ACC_STEPS * n + ep] += 1.0;
+  st.acc[QT_ACC_VIOLATIONS * n + ep] += viol;
+  st.acc[QT_ACC_TERM * n + ep] = term;
+  if (err_out) err_out[ep] = err;
+  if (on_out) on_out[ep] = on;
+  if (done_out) done_out[ep] = term != QT_TERM_RUNNING;
+  if (term_out) term_out[ep] = (int8_t)term;
+  if (viol_out) viol_out[ep] = viol;
+}
+
+// ------------------------------------------------------ controller alone
+
+template <int KC>
+__global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchDev b, const double* __restrict__ obs,
+                                                        double* integ, double* action, int8_t* sat_out,
+                                                        double* diag) {
+  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.n) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  Gains<KC> G;
+  load_gains<KC>(b, ep, G);
+  double qp[3], qv[3], in[3] = {0, 0, 0}, u[4];
+  Target tg;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    qp[i] = obs[i * n + ep];
+    qv[i] = obs[(3 + i) * n + ep];
+    tg.p[i] = obs[(6 + i) * n + ep];
+    tg.v[i] = obs[(9 + i) * n + ep];
+    tg.a[i] = obs[(12 + i) * n + ep];
+  }
+  if (KC == 9) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in[i] = integ[i * n + ep];
+  }
+  const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
+  double dg[16];
+  const bool sat = compute_action<KC, true>(c, G, hover, qp, qv, tg, in, u, dg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
+  if (diag) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) diag[i * n + ep] = dg[i];
+  }
+  if (KC == 9) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) integ[i * n + ep] = in[i];
+  }
+  if (sat_out) sat_out[ep] = sat;
+}
+
+// ---------------------------------------------------------------- target
+
+__global__ __launch_bounds__(kBlock) void target_kernel(qt_env_params e, BatchDev b, const double* __restrict__ t,
+                                                        double* out) {
+  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.n) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  const int motion = motion_of(b, e, ep);
+  const Pattern pt = pattern_of(b, e, motion, ep);
+  Target tg;
+  target_state<true>(e, motion, pt, t[ep], tg);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    out[i * n + ep] = tg.p[i];
+    out[(3 + i) * n + ep] = tg.v[i];
+    out[(6 + i) * n + ep] = tg.a[i];
+  }
+}
+
+// ---------------------------------------------------------------- metrics
+
+// compute_episode_metrics (utils/metrics.py:264-338) from the fused accumulators.
+__global__ __launch_bounds__(kBlock) void metrics_kernel(qt_criteria cr, int64_t n, const double* __restrict__ acc,
+                                                         const double* __restrict__ t, double* met) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  Acc a = load_acc(acc, n, e);
+  double m[QT_MET_ROWS];
+  if (a.steps == 0) {
+#pragma unroll
+    for (int i = 0; i < QT_MET_ROWS; ++i) m[i] = 0.0;
+  } else {
+    // an overshoot still open at the end counts if long enough (metrics.py:256-259)
+    if (a.os_streak >= cr.overshoot_window) {
+      a.os_count += 1;
+      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
+    }
+    if (a.steps < cr.overshoot_window) {  // metrics.py:225-226
+      a.os_count = 0;
+      a.os_max = 0.0;
+    }
+    const double ns = a.steps;
+    const double ratio = a.on_pre / ns;
+    m[QT_MET_DURATION] = t[e];
+    m[QT_MET_ON_TARGET_RATIO] = ratio;
+    m[QT_MET_MEAN_ERR] = a.sum_e / ns;
+    m[QT_MET_MAX_ERR] = a.max_e;
+    m[QT_MET_RMS_ERR] = sqrt(a.sum_e2 / ns);
+    m[QT_MET_TOTAL_EFFORT] = a.sum_u;
+    m[QT_MET_MEAN_EFFORT] = a.sum_u / ns;
+    m[QT_MET_OS_COUNT] = a.os_count;
+    m[QT_MET_OS_MAX] = a.os_max;
+    m[QT_MET_SUCCESS] = (t[e] >= cr.min_episode_duration && ratio >= cr.min_on_target_ratio) ? 1.0 : 0.0;
+    m[QT_MET_TERM] = a.term;
+    m[QT_MET_VIOLATIONS] = a.viol;
+    m[QT_MET_ENV_ON_TARGET_RATIO] = a.on_post / ns;
+    m[QT_MET_STEPS] = ns;
+  }
+#pragma unroll
+  for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
+}
+
+// compute_episode_metrics over recorded arrays (utils/metrics.py:144-338):
+// one lane per episode streams its rows.
+__global__ __launch_bounds__(kBlock) void metrics_arrays_kernel(qt_criteria cr, int64_t n, int32_t max_steps,
+                                                                const double* __restrict__ qpos,
+                                                                const double* __restrict__ tpos,
+                                                                const double* __restrict__ act,
+                                                                const int32_t* __restrict__ steps,
+                                                                const double* __restrict__ last_time,
+                                                                double* met) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  Acc a{0, 0, -INFINITY, 0, 0, 0, 0, 0, 0, -1, -1, 0, 0, 0};
+  const int S = steps[e] < max_steps ? steps[e] : max_steps;
+  const double R = cr.target_radius;
+  for (int s = 0; s < S; ++s) {
+    const int64_t b3 = (int64_t)s * 3 * n + e, b4 = (int64_t)s * 4 * n + e;
+    const double d0 = tpos[b3] - qpos[b3], d1 = tpos[b3 + n] - qpos[b3 + n], d2 = tpos[b3 + 2 * n] - qpos[b3 + 2 * n];
+    const double err = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    a.sum_e += err;
+    a.sum_e2 += err * err;
+    if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;
+    const bool on = err <= R;
+    a.on_pre += on;
+    const double u0 = act[b4], u1 = act[b4 + n], u2 = act[b4 + 2 * n], u3 = act[b4 + 3 * n];
+    a.sum_u += sqrt(u0 * u0 + u1 * u1 + u2 * u2 + u3 * u3);
+    if (a.prev_on >= 0) {
+      overshoot_step(a, on, err - R, cr.overshoot_window);
+    }
+    a.prev_on = on;
+    a.steps += 1;
+  }
+  double m[QT_MET_ROWS];
+#pragma unroll
+  for (int i = 0; i < QT_MET_ROWS; ++i) m[i] = 0.0;
+  if (S > 0) {
+    if (a.os_streak >= cr.overshoot_window) {
+      a.os_count += 1;
+      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
+    }
+    if (S < cr.overshoot_window) {
+      a.os_count = 0;
+      a.os_max = 0.0;
+    }
+    const double ns = S, ratio = a.on_pre / ns, dur = last_time[e];
+    m[QT_MET_DURATION] = dur;
+    m[QT_MET_ON_TARGET_RATIO] = ratio;
+    m[QT_MET_MEAN_ERR] = a.sum_e / ns;
+    m[QT_MET_MAX_ERR] = a.max_e;
+    m[QT_MET_RMS_ERR] = sqrt(a.sum_e2 / ns);
+    m[QT_MET_TOTAL_EFFORT] = a.sum_u;
+    m[QT_MET_MEAN_EFFORT] = a.sum_u / ns;
+    m[QT_MET_OS_COUNT] = a.os_count;
+    m[QT_MET_OS_MAX] = a.os_max;
+    m[QT_MET_SUCCESS] = (dur >= cr.min_episode_duration && ratio >= cr.min_on_target_ratio) ? 1.0 : 0.0;
+    m[QT_MET_STEPS] = ns;
+  }
+#pragma unroll
+  for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
+}
+
+// EvaluationSummary partials (utils/metrics.py:341-390): one workgroup,
+// fixed summation order (bitwise reproducible), first-index argmax/argmin.
+constexpr int kSumBlock = 256;
+__global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const double* __restrict__ met, double mu_r,
+                                                            double mu_e, double* out) {
+  __shared__ double sh[7][kSumBlock];
+  __shared__ double shx[2][kSumBlock];
+  __shared__ int64_t shi[2][kSumBlock];
+  double s[7] = {0, 0, 0, 0, 0, 0, 0};
+  double vmax = -INFINITY, vmin = INFINITY;
+  int64_t imax = -1, imin = -1;
+  for (int64_t e = threadIdx.x; e < n; e += kSumBlock) {
+    const double r = met[QT_MET_ON_TARGET_RATIO * n + e], er = met[QT_MET_MEAN_ERR * n + e];
+    s[0] += r;
+    s[1] += er;
+    s[2] += met[QT_MET_MEAN_EFFORT * n + e];
+    s[3] += met[QT_MET_SUCCESS * n + e];
+    s[4] += 1.0;
+    s[5] += (r - mu_r) * (r - mu_r);
+    s[6] += (er - mu_e) * (er - mu_e);
+    if (r > vmax || imax < 0) vmax = r, imax = e;
+    if (r < vmin || imin < 0) vmin = r, imin = e;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] = s[k];
+  shx[0][threadIdx.x] = vmax;
+  shx[1][threadIdx.x] = vmin;
+  shi[0][threadIdx.x] = imax;
+  shi[1][threadIdx.x] = imin;
+  __syncthreads();
+  for (int w = kSumBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const int o = threadIdx.x + w;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] += sh[k][o];
+      // keep the lowest index among equal values (np.argmax/argmin first occurrence)
+      const int64_t ia = shi[0][threadIdx.x], ib = shi[0][o];
+      if (ib >= 0 && (ia < 0 || shx[0][o] > shx[0][threadIdx.x] ||
+                      (shx[0][o] == shx[0][threadIdx.x] && ib < ia)))
+        shx[0][threadIdx.x] = shx[0][o], shi[0][threadIdx.x] = ib;
+      const int64_t ja = shi[1][threadIdx.x], jb = shi[1][o];
+      if (jb >= 0 && (ja < 0 || shx[1][o] < shx[1][threadIdx.x] ||
+                      (shx[1][o] == shx[1][threadIdx.x] && jb < ja)))
+        shx[1][threadIdx.x] = shx[1][o], shi[1][threadIdx.x] = jb;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) out[k] = sh[k][0];
+    out[7] = shx[0][0];
+    out[8] = (double)shi[0][0];
+    out[9] = shx[1][0];
+    out[10] = (double)shi[1][0];
+  }
+}
+
+BatchDev to_dev(const qt_batch* b) {
+  return BatchDev{b->n, b->motion, b->pattern, b->plant_mass, b->hover_thrust, b->K, b->k_per_episode, b->order};
+}
+
+int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+
+int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
+
+template <int KC, bool FF>
+void launch_rollout_motion(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                           const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
+  switch (motion) {
+    case QT_MOTION_STATIONARY:
+      rollout_kernel<QT_MOTION_STATIONARY, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      break;
+    case QT_MOTION_LINEAR:
+      rollout_kernel<QT_MOTION_LINEAR, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      break;
+    case QT_MOTION_CIRCULAR:
+      rollout_kernel<QT_MOTION_CIRCULAR, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      break;
+    case QT_MOTION_SINUSOIDAL:
+      rollout_kernel<QT_MOTION_SINUSOIDAL, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      break;
+    case QT_MOTION_FIGURE8:
+      rollout_kernel<QT_MOTION_FIGURE8, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      break;
+    default:
+      rollout_kernel<-1, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+  }
+}
+
+bool valid_state(const qt_state& st, bool need_integ) {
+  return st.x && st.t && st.acc && st.target && (!need_integ || st.integ);
+}
+
+}  // namespace
+
+extern "C" {
+
+int qt_abi_version(void) { return QT_ABI_VERSION; }
+
+int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, qt_state st, void* stream) {
+  if (!env || !batch || !offset || batch->n < 0 || !valid_state(st, false)) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;
+  reset_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), offset, st);
+  return check_launch();
+}
+
+int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit, const qt_batch* batch,
+               qt_state st, int32_t nsteps, double* rec, void* stream) {
+  if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
+  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (!valid_state(st, batch->k_cols == 9)) return QT_EINVAL;
+  if (batch->n == 0 || nsteps == 0) return QT_OK;
+  const BatchDev b = to_dev(batch);
+  const int grid = grid_of(batch->n);
+  const int motion = batch->motion ? -1 : env->motion;
+  hipStream_t s = (hipStream_t)stream;
+  const bool ff = ctrl->feedforward_enabled != 0;
+  if (batch->k_cols == 9) {
+    if (ff)
+      launch_rollout_motion<9, true>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    else
+      launch_rollout_motion<9, false>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+  } else {
+    if (ff)
+      launch_rollout_motion<6, true>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    else
+      launch_rollout_motion<6, false>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+  }
+  return check_launch();
+}
+
+int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action, qt_state st, double* err,
+                int8_t* on_target, int8_t* done, int8_t* term, int8_t* violation, void* stream) {
+  if (!env || !batch || !action || batch->n < 0 || !valid_state(st, false)) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;
+  env_step_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), action, st, err,
+                                                                         on_target, done, term, violation);
+  return check_launch();
+}
+
+int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs, double* integ,
+                      double* action, int8_t* saturated, double* diag, void* stream) {
+  if (!ctrl || !batch || !obs || !action || !batch->K || batch->n < 0) return QT_EINVAL;
+  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (batch->k_cols == 9 && !integ) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (batch->k_cols == 9)
+    action_kernel<9><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
+  else
+    action_kernel<6><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
+  return check_launch();
+}
+
+int qt_target_state(const qt_env_params* env, const qt_batch* batch, const double* t, double* out, void* stream) {
+  if (!env || !batch || !t || !out || batch->n < 0) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;
+  target_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), t, out);
+  return check_launch();
+}
+
+int qt_episode_metrics(const qt_criteria* crit, int64_t n, const double* acc, const double* t, double* met,
+                       void* stream) {
+  if (!crit || !acc || !t || !met || n < 0) return QT_EINVAL;
+  if (n == 0) return QT_OK;
+  metrics_kernel<<<grid_of(n), kBlock, 0, (hipStream_t)stream>>>(*crit, n, acc, t, met);
+  return check_launch();
+}
+
+int qt_metrics_from_arrays(const qt_criteria* crit, int64_t n, int32_t max_steps, const double* qpos,
+                           const double* tpos, const double* actions, const int32_t* steps,
+                           const double* last_time, double* met, void* stream) {
+  if (!crit || n < 0 || max_steps < 0 || !steps || !last_time || !met) return QT_EINVAL;
+  if (max_steps > 0 && (!qpos || !tpos || !actions)) return QT_EINVAL;
+  if (n == 0) return QT_OK;
+  metrics_arrays_kernel<<<grid_of(n), kBlock, 0, (hipStream_t)stream>>>(*crit, n, max_steps, qpos, tpos, actions,
+                                                                        steps, last_time, met);
+  return check_launch();
+}
+
+int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, void* stream) {
+  if (!met || !out || n < 0) return QT_EINVAL;
+  summary_kernel<<<1, kSumBlock, 0, (hipStream_t)stream>>>(n, met, mu_ratio, mu_err, out);
+  return check_launch();
+}
+
+}  // extern "C"

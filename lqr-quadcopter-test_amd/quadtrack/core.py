@@ -1,0 +1,250 @@
+"""Device-side batch containers and thin launchers over the C ABI.
+
+All arrays are structure-of-arrays float64 tensors in HBM ([rows][n], one
+column per episode), the layout the kernels read coalesced (one lane per
+episode).  Every launcher is asynchronous on the current torch stream of the
+batch's device.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import ACC_ROWS, MET_ROWS, Batch, Criteria, CtrlParams, EnvParams, State, check, ptr, stream_of
+
+F64 = torch.float64
+
+
+def criteria(min_on_target_ratio=0.8, min_episode_duration=30.0, target_radius=0.5, window=10) -> Criteria:
+    """utils/metrics.py SuccessCriteria defaults (26-39) + detect_overshoots window (208)."""
+    return Criteria(float(min_on_target_ratio), float(min_episode_duration), float(target_radius), int(window), 0)
+
+
+@dataclass
+class EpisodeBatch:
+    """Per-episode inputs (qt_batch)."""
+
+    n: int
+    device: torch.device
+    pattern: torch.Tensor                     # [4, n] raw draws
+    offset: torch.Tensor                      # [3, n]
+    K: torch.Tensor                           # [4*k_cols, n] or [4*k_cols, 1]
+    k_cols: int
+    motion: torch.Tensor | None = None        # [n] int8
+    plant_mass: torch.Tensor | None = None    # [n]
+    hover: torch.Tensor | None = None         # [n]
+    order: torch.Tensor | None = None         # [n] int32
+
+    def c_batch(self, with_k=True) -> Batch:
+        b = Batch()
+        b.n = self.n
+        b.motion = ptr(self.motion)
+        b.pattern = ptr(self.pattern)
+        b.plant_mass = ptr(self.plant_mass)
+        b.hover_thrust = ptr(self.hover)
+        b.K = ptr(self.K) if with_k else None
+        b.k_cols = self.k_cols
+        b.k_per_episode = int(self.K.shape[1] != 1)
+        b.order = ptr(self.order)
+        return b
+
+
+@dataclass
+class RolloutState:
+    """Mutable per-episode state (qt_state)."""
+
+    x: torch.Tensor       # [12, n]
+    integ: torch.Tensor   # [3, n]
+    t: torch.Tensor       # [n]
+    acc: torch.Tensor     # [ACC_ROWS, n]
+    target: torch.Tensor  # [9, n]
+
+    @classmethod
+    def empty(cls, n: int, device) -> "RolloutState":
+        z = lambda *s: torch.zeros(*s, dtype=F64, device=device)  # noqa: E731
+        return cls(z(12, n), z(3, n), z(n), z(ACC_ROWS, n), z(9, n))
+
+    def c_state(self) -> State:
+        s = State()
+        s.x, s.integ, s.t, s.acc, s.target = (ptr(v) for v in (self.x, self.integ, self.t, self.acc, self.target))
+        return s
+
+
+def to_device(a, device, dtype=F64) -> torch.Tensor:
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device).contiguous()
+
+
+def _check_cols(name, t, rows, n):
+    if t is not None and (t.dim() != 2 or t.shape[0] != rows or t.shape[1] != n or not t.is_contiguous()):
+        raise ValueError(f"{name} must be a contiguous [{rows}, {n}] tensor, got {tuple(t.shape)}")
+
+
+def validate(batch: EpisodeBatch, st: RolloutState | None = None):
+    """Host-side shape checks before any launch (the kernels index [rows][n])."""
+    n = batch.n
+    _check_cols("pattern", batch.pattern, 4, n)
+    _check_cols("offset", batch.offset, 3, n)
+    if batch.k_cols not in (6, 9):
+        raise ValueError("k_cols must be 6 or 9")
+    if batch.K.dim() != 2 or batch.K.shape[0] != 4 * batch.k_cols or batch.K.shape[1] not in (1, n):
+        raise ValueError(f"K must be [{4 * batch.k_cols}, 1 or {n}], got {tuple(batch.K.shape)}")
+    for name in ("motion", "plant_mass", "hover", "order"):
+        t = getattr(batch, name)
+        if t is not None and (t.numel() != n or not t.is_contiguous()):
+            raise ValueError(f"{name} must have {n} contiguous entries")
+    if batch.motion is not None and (int(batch.motion.min()) < 0 or int(batch.motion.max()) > 4):
+        raise ValueError("motion types must be in 0..4")
+    if batch.order is not None:
+        o = batch.order.to(torch.int64)
+        if int(o.min()) < 0 or int(o.max()) >= n:
+            raise ValueError("order entries out of range")
+    if st is not None:
+        _check_cols("x", st.x, 12, n)
+        _check_cols("integ", st.integ, 3, n)
+        _check_cols("acc", st.acc, ACC_ROWS, n)
+        _check_cols("target", st.target, 9, n)
+        if st.t.numel() != n:
+            raise ValueError("t must have n entries")
+    for t in (batch.pattern, batch.offset, batch.K):
+        if t.device != batch.device or t.dtype != F64:
+            raise ValueError("batch tensors must be float64 on the batch device")
+
+
+def reset(env: EnvParams, batch: EpisodeBatch, st: RolloutState):
+    lib = _abi.load()
+    with torch.cuda.device(batch.device):
+        check(lib.qt_reset(C.byref(env), C.byref(batch.c_batch(with_k=False)), ptr(batch.offset), st.c_state(),
+                           stream_of(batch.device)), "qt_reset")
+
+
+def rollout(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState, nsteps: int,
+            rec: torch.Tensor | None = None):
+    lib = _abi.load()
+    if rec is not None and (rec.numel() < nsteps * 16 * batch.n or rec.dtype != F64):
+        raise ValueError("rec must hold nsteps * 16 * n float64")
+    with torch.cuda.device(batch.device):
+        check(lib.qt_rollout(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()), st.c_state(),
+                             int(nsteps), ptr(rec), stream_of(batch.device)), "qt_rollout")
+
+
+def episode_metrics(crit: Criteria, st: RolloutState) -> torch.Tensor:
+    lib = _abi.load()
+    n = st.t.numel()
+    met = torch.empty(MET_ROWS, n, dtype=F64, device=st.t.device)
+    with torch.cuda.device(st.t.device):
+        check(lib.qt_episode_metrics(C.byref(crit), n, ptr(st.acc), ptr(st.t), ptr(met), stream_of(st.t.device)),
+              "qt_episode_metrics")
+    return met
+
+
+def summary_partials(met: torch.Tensor, mu_ratio=0.0, mu_err=0.0) -> torch.Tensor:
+    """[sum ratio, sum err, sum effort, sum success, count, M2 ratio, M2 err, max, argmax, min, argmin]."""
+    lib = _abi.load()
+    out = torch.zeros(11, dtype=F64, device=met.device)
+    with torch.cuda.device(met.device):
+        check(lib.qt_summary(met.shape[1], ptr(met), float(mu_ratio), float(mu_err), ptr(out),
+                             stream_of(met.device)), "qt_summary")
+    return out
+
+
+def dare_batched(n_state: int, dt: float, gravity: float, mass: torch.Tensor | None, Q: torch.Tensor,
+                 R: torch.Tensor, structured: bool):
+    """Q [n_state*n_state, m], R [16, m] SoA -> (K [4*n_state, m], P [n_state^2, m], status int8 [m], iters int32 [m])."""
+    lib = _abi.load()
+    m = Q.shape[1]
+    dev = Q.device
+    if Q.shape[0] != n_state * n_state or R.shape != (16, m):
+        raise ValueError("Q must be [n*n, m] and R [16, m]")
+    if mass is not None and mass.numel() != m:
+        raise ValueError("mass must have m entries")
+    K = torch.empty(4 * n_state, m, dtype=F64, device=dev)
+    P = torch.empty(n_state * n_state, m, dtype=F64, device=dev)
+    status = torch.empty(m, dtype=torch.int8, device=dev)
+    iters = torch.empty(m, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_dare_batched(n_state, m, float(dt), float(gravity), ptr(mass), ptr(Q), ptr(R), int(structured),
+                                  ptr(K), ptr(P), ptr(status), ptr(iters), stream_of(dev)), "qt_dare_batched")
+    return K, P, status, iters
+
+
+def dare_dense(A: torch.Tensor, B: torch.Tensor, Q: torch.Tensor, R: torch.Tensor, ab_per_problem: bool):
+    """General DARE: A [n*n, m'], B [n*p, m'], Q [n*n, m], R [p*p, m] SoA (m' = m or 1)."""
+    lib = _abi.load()
+    m = Q.shape[1]
+    n = int(round(Q.shape[0] ** 0.5))
+    p = int(round(R.shape[0] ** 0.5))
+    dev = Q.device
+    K = torch.empty(p * n, m, dtype=F64, device=dev)
+    P = torch.empty(n * n, m, dtype=F64, device=dev)
+    status = torch.empty(m, dtype=torch.int8, device=dev)
+    iters = torch.empty(m, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_dare_dense(n, p, m, ptr(A), ptr(B), int(ab_per_problem), ptr(Q), ptr(R), ptr(K), ptr(P),
+                                ptr(status), ptr(iters), stream_of(dev)), "qt_dare_dense")
+    return K, P, status, iters
+
+
+def target_state(env: EnvParams, batch: EpisodeBatch, t: torch.Tensor) -> torch.Tensor:
+    lib = _abi.load()
+    out = torch.empty(9, batch.n, dtype=F64, device=batch.device)
+    with torch.cuda.device(batch.device):
+        check(lib.qt_target_state(C.byref(env), C.byref(batch.c_batch(with_k=False)), ptr(t), ptr(out),
+                                  stream_of(batch.device)), "qt_target_state")
+    return out
+
+
+def env_step(env: EnvParams, batch: EpisodeBatch, action: torch.Tensor, st: RolloutState):
+    """Open-loop step; returns (err[n], on_target[n] bool, done[n] bool, term[n] int8, violation[n] bool)."""
+    lib = _abi.load()
+    n, dev = batch.n, batch.device
+    _check_cols("action", action, 4, n)
+    err = torch.empty(n, dtype=F64, device=dev)
+    on = torch.empty(n, dtype=torch.int8, device=dev)
+    done = torch.empty(n, dtype=torch.int8, device=dev)
+    term = torch.empty(n, dtype=torch.int8, device=dev)
+    viol = torch.empty(n, dtype=torch.int8, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_env_step(C.byref(env), C.byref(batch.c_batch(with_k=False)), ptr(action), st.c_state(), ptr(err),
+                              ptr(on), ptr(done), ptr(term), ptr(viol), stream_of(dev)), "qt_env_step")
+    return err, on.bool(), done.bool(), term, viol.bool()
+
+
+def compute_action(ctrl: CtrlParams, K: torch.Tensor, k_cols: int, obs: torch.Tensor, integ: torch.Tensor,
+                   hover: torch.Tensor | None = None, diag: torch.Tensor | None = None):
+    """obs [15, n] -> (action [4, n], saturated [n] bool); integ [3, n] updated in place (LQI);
+    diag [16, n] (optional) receives the control components."""
+    lib = _abi.load()
+    n, dev = obs.shape[1], obs.device
+    _check_cols("obs", obs, 15, n)
+    b = Batch()
+    b.n = n
+    b.K = ptr(K)
+    b.k_cols = k_cols
+    b.k_per_episode = int(K.shape[1] != 1)
+    b.hover_thrust = ptr(hover)
+    act = torch.empty(4, n, dtype=F64, device=dev)
+    sat = torch.empty(n, dtype=torch.int8, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_compute_action(C.byref(ctrl), C.byref(b), ptr(obs), ptr(integ), ptr(act), ptr(sat), ptr(diag),
+                                    stream_of(dev)), "qt_compute_action")
+    return act, sat.bool()
+
+
+def metrics_from_arrays(crit: Criteria, qpos: torch.Tensor, tpos: torch.Tensor, actions: torch.Tensor,
+                        steps: torch.Tensor, last_time: torch.Tensor) -> torch.Tensor:
+    """qpos/tpos [S, 3, n], actions [S, 4, n], steps int32 [n], last_time [n] -> met [MET_ROWS, n]."""
+    lib = _abi.load()
+    S, _, n = qpos.shape
+    dev = qpos.device
+    met = torch.empty(MET_ROWS, n, dtype=F64, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_metrics_from_arrays(C.byref(crit), n, S, ptr(qpos), ptr(tpos), ptr(actions), ptr(steps),
+                                         ptr(last_time), ptr(met), stream_of(dev)), "qt_metrics_from_arrays")
+    return met

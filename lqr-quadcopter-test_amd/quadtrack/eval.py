@@ -1,0 +1,156 @@
+"""Evaluation drivers — drop-in `Evaluator` / `load_controller` of the
+reference's `quadcopter_tracking.eval` (eval.py:59-513) plus the batched
+evaluator that replaces its per-episode loop.
+
+* `Evaluator.run_episode` / `evaluate` keep the reference semantics exactly,
+  including the controller NOT being reset between episodes (eval.py:95-206;
+  SURVEY F8: the LQI integral carries over), stepping the GPU-backed
+  `QuadcopterEnv` and controller one step at a time.
+* `evaluate_batched` runs all episodes at once in the fused closed-loop
+  kernel with a fresh controller per episode (the tuner / trainer semantics,
+  controllers/tuning.py:879, train.py:594) and returns the same
+  `EvaluationSummary`.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+from copy import deepcopy
+from datetime import datetime, timezone
+from pathlib import Path
+from typing import Callable
+
+import numpy as np
+
+from .controllers import BaseController, BatchedRiccatiLQR, LQRController, RiccatiLQRController
+from .env import EnvConfig, QuadcopterEnv
+from .env.config import as_env_config
+from .rollout import run_closed_loop
+from .utils.metrics import (
+    EvaluationSummary,
+    SuccessCriteria,
+    compute_episode_metrics,
+    compute_evaluation_summary,
+    format_metrics_report,
+)
+
+logger = logging.getLogger(__name__)
+
+
+class Evaluator:
+    """Controller evaluation pipeline (eval.py:59-268, plots excluded)."""
+
+    def __init__(self, controller: BaseController, env_config: EnvConfig | None = None,
+                 criteria: SuccessCriteria | None = None, output_dir: str | Path = "reports"):
+        self.controller = controller
+        self.env_config = env_config or EnvConfig()
+        self.criteria = criteria or SuccessCriteria()
+        self.output_dir = Path(output_dir)
+        self.output_dir.mkdir(parents=True, exist_ok=True)
+        (self.output_dir / "plots").mkdir(exist_ok=True)
+        self.episode_data_list: list[list[dict]] = []
+        self.episode_info_list: list[dict] = []
+
+    def run_episode(self, seed: int, max_steps: int | None = None,
+                    progress_callback: Callable | None = None) -> tuple[list[dict], dict]:
+        env = QuadcopterEnv(config=self.env_config)
+        obs = env.reset(seed=seed)
+        episode_data: list[dict] = []
+        done = False
+        step = 0
+        info: dict = {}
+        while not done:
+            if max_steps is not None and step >= max_steps:
+                break
+            try:
+                action = self.controller.compute_action(obs)
+            except Exception as e:  # eval.py:124-136
+                logger.error("Controller error at step %d: %s", step, e)
+                info = {"termination_reason": "controller_error", "time": step * env.dt, "tracking_error": 0.0,
+                        "on_target": False, "on_target_ratio": 0.0, "action_violations": 0}
+                break
+            next_obs, reward, done, info = env.step(action)
+            episode_data.append({
+                "time": info.get("time", step * env.dt), "step": step,
+                "quadcopter_position": obs["quadcopter"]["position"].tolist(),
+                "quadcopter_velocity": obs["quadcopter"]["velocity"].tolist(),
+                "target_position": obs["target"]["position"].tolist(),
+                "target_velocity": obs["target"]["velocity"].tolist(),
+                "action": [action["thrust"], action["roll_rate"], action["pitch_rate"], action["yaw_rate"]],
+                "reward": reward, "tracking_error": info.get("tracking_error", 0.0),
+                "on_target": info.get("on_target", False),
+            })
+            obs = next_obs
+            step += 1
+            if progress_callback and step % 100 == 0:
+                progress_callback(step, info)
+        return episode_data, info
+
+    def evaluate(self, num_episodes: int = 10, base_seed: int = 42, max_steps_per_episode: int | None = None,
+                 verbose: bool = True) -> EvaluationSummary:
+        self.episode_data_list, self.episode_info_list = [], []
+        metrics = []
+        for i in range(num_episodes):
+            data, info = self.run_episode(seed=base_seed + i, max_steps=max_steps_per_episode)
+            self.episode_data_list.append(data)
+            self.episode_info_list.append(info)
+            m = compute_episode_metrics(data, self.criteria, info)
+            metrics.append(m)
+            if verbose:
+                logger.info("  %s | on-target: %.1f%% | error: %.3fm | duration: %.1fs",
+                            "SUCCESS" if m.success else "FAILED", m.on_target_ratio * 100, m.mean_tracking_error,
+                            m.episode_duration)
+        summary = compute_evaluation_summary(metrics, self.criteria)
+        if verbose:
+            print("\n" + format_metrics_report(summary))
+        return summary
+
+    def save_report(self, summary: EvaluationSummary, experiment_name: str | None = None) -> dict[str, Path]:
+        """metrics.json + text report (eval.py:233-268)."""
+        if experiment_name is None:
+            stamp = datetime.now(timezone.utc).strftime("%Y%m%d_%H%M%S")
+            experiment_name = f"eval_{self.controller.name}_{stamp}"
+        paths = {"metrics": self.output_dir / "metrics.json", "report": self.output_dir / f"{experiment_name}_report.txt"}
+        paths["metrics"].write_text(json.dumps(summary.to_dict(), indent=2))
+        paths["report"].write_text(format_metrics_report(summary))
+        return paths
+
+
+def load_controller(controller_type: str, checkpoint_path=None, config: dict | None = None) -> BaseController:
+    """Controller factory (eval.py:472-513) for the controllers on this path."""
+    config = config or {}
+    if controller_type == "lqr":
+        return LQRController(config=config)
+    if controller_type == "riccati_lqr":
+        return RiccatiLQRController(config=config)
+    if controller_type == "lqi":
+        cfg = deepcopy(config)
+        cfg["use_lqi"] = True
+        cfg.setdefault("q_int", [0.01, 0.01, 0.1])
+        return RiccatiLQRController(config=cfg)
+    if controller_type in ("deep", "pid"):
+        raise NotImplementedError(f"controller type '{controller_type}' is outside the MI355X hot path")
+    raise ValueError(f"Unknown controller type: {controller_type}")
+
+
+def evaluate_batched(controller, env_config=None, num_episodes: int = 10, base_seed: int = 42,
+                     criteria: SuccessCriteria | None = None, motion=None, plant_mass=None,
+                     max_steps_per_episode: int | None = None, with_episode_metrics: bool = True,
+                     group=None, global_offset: int = 0) -> EvaluationSummary:
+    """All episodes in one fused closed-loop launch (fresh controller each).
+
+    `controller` is a RiccatiLQRController (shared gains), a
+    BatchedRiccatiLQR (shared or per-episode gains) or a config dict."""
+    cfg = as_env_config(env_config)
+    if isinstance(controller, dict):
+        controller = BatchedRiccatiLQR(controller)
+    elif isinstance(controller, RiccatiLQRController):
+        controller = controller.to_batched()
+    seeds = base_seed + global_offset + np.arange(num_episodes)
+    res = run_closed_loop(controller, cfg, n=num_episodes, seeds=seeds, motion=motion, plant_mass=plant_mass,
+                          criteria=criteria, max_steps=max_steps_per_episode)
+    summary = res.summary(group=group, global_offset=global_offset)
+    if with_episode_metrics:
+        summary.episode_metrics = res.episode_metrics()
+    return summary

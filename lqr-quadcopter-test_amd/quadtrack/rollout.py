@@ -1,0 +1,148 @@
+"""The fused batched closed loop: N independent episodes of
+`RiccatiLQRController.compute_action` -> `QuadcopterEnv.step` in one kernel.
+
+This is what the reference's per-episode Python loops do one step at a time
+(eval.py:95-167 `Evaluator.run_episode`, controllers/tuning.py:874-906
+`ControllerTuner._evaluate_config`, train.py:588-638 classical epochs): here
+every episode is one GPU lane, the whole 30 s episode runs register-resident
+inside `qt_rollout`, and the Evaluator's per-episode metrics are accumulated
+in the same pass (no per-step data leaves the chip).
+
+Semantics: each episode uses a fresh controller (integral zeroed at reset),
+as the tuner and trainer do (tuning.py:879, train.py:594); see SURVEY F8 for
+the Evaluator's carry-over, which `quadtrack.eval.Evaluator` reproduces.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _abi, core
+from ._abi import MET, MET_FIELDS, TERM_REASONS
+from .controllers.riccati_lqr import BatchedRiccatiLQR
+from .env import seeding
+from .env.batched import motion_indices
+from .env.config import as_env_config
+
+F64 = torch.float64
+
+
+def max_steps_for(env_params) -> int:
+    """Upper bound on steps before `t >= max_episode_time` (t accumulates dt)."""
+    return int(math.ceil(env_params.max_episode_time / env_params.dt)) + 2
+
+
+@dataclass
+class RolloutResult:
+    metrics: torch.Tensor            # [MET_ROWS, n] float64 (EpisodeMetrics fields, include/quadtrack.h)
+    state: core.RolloutState
+    batch: core.EpisodeBatch
+    criteria: object
+    record: torch.Tensor | None = None  # [steps, 16, n]: state after step + applied action
+
+    @property
+    def n(self) -> int:
+        return self.metrics.shape[1]
+
+    def metric(self, name: str) -> torch.Tensor:
+        return self.metrics[MET[name]]
+
+    def final_state(self) -> torch.Tensor:
+        return self.state.x.T.clone()
+
+    def episode_metrics(self):
+        """List of utils.metrics.EpisodeMetrics (host copies)."""
+        from .utils.metrics import EpisodeMetrics
+
+        m = self.metrics.cpu().numpy()
+        out = []
+        for e in range(m.shape[1]):
+            row = dict(zip(MET_FIELDS, m[:, e]))
+            out.append(EpisodeMetrics(
+                episode_duration=float(row["episode_duration"]), on_target_ratio=float(row["on_target_ratio"]),
+                mean_tracking_error=float(row["mean_tracking_error"]),
+                max_tracking_error=float(row["max_tracking_error"]),
+                rms_tracking_error=float(row["rms_tracking_error"]),
+                total_control_effort=float(row["total_control_effort"]),
+                mean_control_effort=float(row["mean_control_effort"]),
+                overshoot_count=int(row["overshoot_count"]), max_overshoot=float(row["max_overshoot"]),
+                success=bool(row["success"]), termination_reason=TERM_REASONS[int(row["termination_code"])],
+                action_violations=int(row["action_violations"])))
+        return out
+
+    def summary(self, group=None, global_offset: int = 0):
+        """EvaluationSummary over all episodes (utils/metrics.py:341-390); with
+        torch.distributed initialised, reduced over every rank's shard."""
+        from .parallel import reduce_summary
+
+        return reduce_summary(self.metrics, self.criteria, group=group, global_offset=global_offset)
+
+
+def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, motion=None, plant_mass=None,
+                draws=None, device=None, order=None) -> core.EpisodeBatch:
+    cfg = as_env_config(env_config)
+    dev = _abi.require_gpu(device if device is not None else controller.device)
+    if controller.per_episode and controller.num_problems != n:
+        raise ValueError(f"controller has {controller.num_problems} gain sets for {n} episodes")
+    if draws is None:
+        if seeds is None:
+            seeds = np.arange(n)
+        seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
+        if seeds.size != n:
+            raise ValueError(f"{seeds.size} seeds for {n} episodes")
+        kinds = motion_indices(motion, n) if motion is not None else cfg.motion_index()
+        draws = seeding.draws(kinds, seeds)
+    pat, off = draws
+    mo = None if motion is None else torch.as_tensor(motion_indices(motion, n), device=dev)
+    pm = None if plant_mass is None else core.to_device(np.broadcast_to(np.asarray(plant_mass, float), (n,)), dev)
+    od = None if order is None else torch.as_tensor(np.asarray(order, dtype=np.int32), device=dev)
+    b = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pat, dev), offset=core.to_device(off, dev),
+                          K=controller.K, k_cols=controller.k_cols, motion=mo, plant_mass=pm, hover=controller.hover,
+                          order=od)
+    return b
+
+
+def run_closed_loop(controller: BatchedRiccatiLQR, env_config=None, n: int | None = None, seeds=None, motion=None,
+                    plant_mass=None, criteria=None, draws=None, max_steps: int | None = None, chunk: int | None = None,
+                    record: bool = False, batch: core.EpisodeBatch | None = None) -> RolloutResult:
+    """Run `n` closed-loop episodes to termination (or `max_steps`).
+
+    seeds     per-episode reset seeds (default 0..n-1); draws=(pattern, offset) overrides them
+    motion    per-episode motion types (default: the config's)
+    plant_mass per-episode plant mass (controller masses are the controller's)
+    criteria  the Evaluator's SuccessCriteria (default utils.metrics defaults)
+    chunk     steps per kernel launch (default: the whole episode in one launch)
+    record    keep every step's state and action ([steps, 16, n]; for parity tests)
+    """
+    cfg = as_env_config(env_config)
+    env = cfg.to_params()
+    if n is None:
+        n = controller.num_problems if controller.per_episode else (len(seeds) if seeds is not None else 1)
+    if batch is None:
+        batch = build_batch(controller, cfg, n, seeds=seeds, motion=motion, plant_mass=plant_mass, draws=draws)
+    crit = _criteria(criteria)
+    st = core.RolloutState.empty(n, batch.device)
+    core.validate(batch, st)
+    core.reset(env, batch, st)
+    total = max_steps if max_steps is not None else max_steps_for(env)
+    step = chunk or total
+    rec = torch.full((total, 16, n), float("nan"), dtype=F64, device=batch.device) if record else None
+    done = 0
+    while done < total:
+        k = min(step, total - done)
+        core.rollout(env, controller.ctrl, crit, batch, st, k, None if rec is None else rec[done:done + k])
+        done += k
+    met = core.episode_metrics(crit, st)
+    return RolloutResult(metrics=met, state=st, batch=batch, criteria=crit, record=rec)
+
+
+def _criteria(criteria):
+    if criteria is None:
+        return core.criteria()
+    if isinstance(criteria, _abi.Criteria):
+        return criteria
+    return core.criteria(criteria.min_on_target_ratio, criteria.min_episode_duration, criteria.target_radius)

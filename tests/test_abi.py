@@ -1,0 +1,93 @@
+"""C-ABI checks that need no GPU: the library loads, exports every entry point
+include/quadtrack.h declares, and the ctypes structs have the C layout."""
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+from quadtrack import _abi
+
+HEADER = os.path.join(ROOT, "include", "quadtrack.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^int (qt_\w+)\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    assert set(declared_functions()) == set(_abi.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.qt_abi_version() == _abi.ABI_VERSION
+    nm = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r" T (qt_\w+)", nm.stdout))
+    assert set(declared_functions()) <= exported
+
+
+PROBE = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "quadtrack.h"
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("qt_env_params %zu\nqt_ctrl_params %zu\nqt_criteria %zu\nqt_batch %zu\nqt_state %zu\n",
+         sizeof(qt_env_params), sizeof(qt_ctrl_params), sizeof(qt_criteria), sizeof(qt_batch), sizeof(qt_state));
+  F(qt_env_params, integrator) F(qt_env_params, motion) F(qt_env_params, speed) F(qt_env_params, center)
+  F(qt_env_params, min_episode_duration) F(qt_ctrl_params, use_lqi) F(qt_ctrl_params, integral_limit)
+  F(qt_ctrl_params, ff_max_acceleration) F(qt_criteria, overshoot_window) F(qt_batch, K) F(qt_batch, k_cols)
+  F(qt_batch, order) F(qt_state, target)
+  printf("QT_ACC_ROWS %d\nQT_MET_ROWS %d\n", QT_ACC_ROWS, QT_MET_ROWS);
+  return 0;
+}
+"""
+
+
+def test_struct_layout_matches_c(tmp_path):
+    src = tmp_path / "probe.c"
+    src.write_text(PROBE)
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                              check=True).stdout.strip().splitlines())
+    cls = {"qt_env_params": _abi.EnvParams, "qt_ctrl_params": _abi.CtrlParams, "qt_criteria": _abi.Criteria,
+           "qt_batch": _abi.Batch, "qt_state": _abi.State}
+    for k, v in out.items():
+        if k in cls:
+            assert C.sizeof(cls[k]) == int(v), k
+        elif "." in k:
+            s, f = k.split(".")
+            assert getattr(cls[s], f).offset == int(v), k
+    assert int(out["QT_ACC_ROWS"]) == _abi.ACC_ROWS
+    assert int(out["QT_MET_ROWS"]) == _abi.MET_ROWS
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_abi.QuadtrackError):
+        _abi.require_gpu()
+    from quadtrack import BatchedQuadcopterEnv, RiccatiLQRController
+
+    with pytest.raises(_abi.QuadtrackError):
+        BatchedQuadcopterEnv(4)
+    with pytest.raises(_abi.QuadtrackError):
+        RiccatiLQRController({"dt": 0.01})
+
+
+def test_kernels_built_for_gfx950():
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", _abi.LIB_PATH], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    assert "gfx950" in out.stdout

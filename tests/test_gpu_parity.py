@@ -1,0 +1,429 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference's
+golden fixtures and the CPU oracle on identical seeded inputs.
+
+Tolerance (north star): 1e-5 absolute on states and per-episode metrics in
+FP64.  Exceptions, both inherited from the reference's own numerics:
+figure-8 feed-forward runs (1e-6 finite-difference acceleration, ~1e-4
+noise) and the sub-ulp DARE differences between scipy's QZ solver and the
+doubling algorithm (gains compared at rtol 1e-8).
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SCEN = json.load(open(os.path.join(GOLDEN, "scenarios.json")))
+CL = np.load(os.path.join(GOLDEN, "closed_loop.npz"))
+FIELDS = SCEN["metric_fields"]
+TOL = 1e-5
+FF_FIG8_TOL = 2e-3
+
+
+@pytest.fixture(scope="module")
+def qt():
+    import quadtrack
+
+    quadtrack._abi.require_gpu()
+    return quadtrack
+
+
+def _cfg_list(s, key, n):
+    per = s.get(f"{key}_per_episode")
+    return per if per is not None else [s[key]] * n
+
+
+# ------------------------------------------------------------ closed loop
+
+
+@pytest.mark.parametrize("s", SCEN["scenarios"], ids=[s["name"] for s in SCEN["scenarios"]])
+def test_fused_rollout_matches_reference(qt, s):
+    """Per-scenario batch through qt_reset + qt_rollout + qt_episode_metrics."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = len(s["seeds"])
+    envs, ctls = _cfg_list(s, "env", n), _cfg_list(s, "ctl", n)
+    tol = FF_FIG8_TOL if s["name"] == "ff_figure8" else TOL
+    # one batch per distinct env config (config 5 varies motion and mass per episode)
+    base_env = json.loads(json.dumps(envs[0]))
+    base_env.pop("quadcopter", None)
+    base_env.setdefault("target", {}).pop("motion_type", None)
+    uniform_env = all(json.dumps(e, sort_keys=True) == json.dumps(envs[0], sort_keys=True) for e in envs)
+    motion = None if uniform_env else [e["target"]["motion_type"] for e in envs]
+    plant_mass = None if uniform_env else [e.get("quadcopter", {}).get("mass", 1.0) for e in envs]
+    env_cfg = envs[0] if uniform_env else base_env
+    if all(json.dumps(c, sort_keys=True) == json.dumps(ctls[0], sort_keys=True) for c in ctls):
+        ctl = BatchedRiccatiLQR(ctls[0])
+    else:
+        keys = {k for c in ctls for k in c}
+        per = {k: [c[k] for c in ctls] for k in ("q_pos", "q_vel", "r_controls", "mass") if k in keys}
+        shared = {k: v for k, v in ctls[0].items() if k not in per}
+        ctl = BatchedRiccatiLQR(shared, **per)
+    res = run_closed_loop(ctl, env_cfg, n=n, seeds=s["seeds"], motion=motion, plant_mass=plant_mass,
+                          record=s["record"], chunk=777)
+    met = res.metrics.cpu().numpy()
+    ref = CL[s["name"] + "_metrics"]
+    for i, f in enumerate(FIELDS):
+        np.testing.assert_allclose(met[i], ref[:, i], rtol=1e-8, atol=tol, err_msg=f)
+    fin = CL[s["name"] + "_final"]
+    np.testing.assert_allclose(res.state.x.cpu().numpy().T, fin[:, :12], rtol=1e-8, atol=tol)
+    if ctl.use_lqi:
+        np.testing.assert_allclose(res.state.integ.cpu().numpy().T, fin[:, 12:], rtol=1e-8, atol=tol)
+    if s["record"]:
+        rec = res.record.cpu().numpy()  # [steps, 16, n]
+        steps = CL["rec_steps"]
+        for e in range(n):
+            ok = steps < int(ref[e, FIELDS.index("steps")])
+            np.testing.assert_allclose(rec[steps[ok], :12, e], CL[s["name"] + "_rec_state"][e][ok], rtol=1e-8,
+                                       atol=tol)
+            np.testing.assert_allclose(rec[steps[ok], 12:, e], CL[s["name"] + "_rec_action"][e][ok], rtol=1e-8,
+                                       atol=tol)
+
+
+def test_config1_plumbing(qt):
+    """Config 1 through the drop-in single-episode classes, step by step."""
+    from quadtrack import QuadcopterEnv, RiccatiLQRController
+    from quadtrack.utils.metrics import compute_episode_metrics
+
+    env = QuadcopterEnv({"logging": {"enabled": False}})
+    ctl = RiccatiLQRController({"dt": 0.01})
+    obs = env.reset(seed=0)
+    data, done, info = [], False, {}
+    while not done:
+        a = ctl.compute_action(obs)
+        nobs, r, done, info = env.step(a)
+        data.append({"time": info["time"], "quadcopter_position": obs["quadcopter"]["position"].tolist(),
+                     "target_position": obs["target"]["position"].tolist(),
+                     "action": [a["thrust"], a["roll_rate"], a["pitch_rate"], a["yaw_rate"]]})
+        obs = nobs
+    m = compute_episode_metrics(data, None, info)
+    assert len(data) == 3000 and info["termination_reason"] == "time_limit"
+    assert m.mean_tracking_error == pytest.approx(0.1090241018, abs=1e-9)
+    assert m.on_target_ratio == pytest.approx(0.992333, abs=1e-6)
+    assert info["on_target_ratio"] == pytest.approx(0.992667, abs=1e-6)
+    np.testing.assert_allclose(env.get_state_vector()[:3], [0.0673493918, -0.1132311124, 0.9999439135], atol=1e-9)
+
+
+# --------------------------------------------------------- full-size batch
+
+
+def test_full_batch_65536_linear_vs_oracle(qt):
+    """Config 2 at full size on the GPU; a seeded sample of 512 episodes is
+    recomputed by the oracle, and the size-independent properties are checked
+    on all 65,536."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = 65536
+    cfg = {"target": {"motion_type": "linear"}}
+    res = run_closed_loop(BatchedRiccatiLQR({"dt": 0.01}), cfg, n=n, seeds=np.arange(n))
+    met = res.metrics.cpu().numpy()
+    assert np.all(met[FIELDS.index("steps")] == 3000)
+    assert np.all(met[FIELDS.index("termination_code")] == 1)
+    assert np.all(np.isfinite(met))
+    r = met[FIELDS.index("rms_tracking_error")]
+    assert np.all(r >= met[FIELDS.index("mean_tracking_error")] - 1e-12)
+    assert np.all(met[FIELDS.index("max_tracking_error")] >= r - 1e-12)
+    sample = np.random.default_rng(7).choice(n, 512, replace=False)
+    env = O.env_params(cfg)
+    c, K, kc, _, _ = O.controller({"dt": 0.01})
+    pat, off = O.draws("linear", sample)
+    x0 = np.array([O.initial_state(env, 1, pat[i], off[i]) for i in range(len(sample))])
+    om, oxf, _, _ = O.rollout(env, c, O.criteria(), None, pat, None, None, K, kc, False, x0)
+    np.testing.assert_allclose(met[:, sample].T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(res.state.x.cpu().numpy()[:, sample].T, oxf, rtol=1e-8, atol=TOL)
+
+
+def test_chunked_equals_single_launch(qt):
+    """Idempotence of chunking: 3000 steps in one launch == 7 uneven chunks."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    ctl = BatchedRiccatiLQR({"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]})
+    a = run_closed_loop(ctl, {"target": {"motion_type": "sinusoidal"}}, n=1000, seeds=np.arange(1000))
+    b = run_closed_loop(ctl, {"target": {"motion_type": "sinusoidal"}}, n=1000, seeds=np.arange(1000), chunk=431)
+    assert torch.equal(a.metrics, b.metrics)
+    assert torch.equal(a.state.x, b.state.x)
+
+
+def test_mixed_motion_order_permutation(qt):
+    """A per-episode `order` (group episodes by motion) does not change results."""
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch, run_closed_loop
+
+    n = 2000
+    motion = [i % 5 for i in range(n)]
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    a = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
+    order = np.argsort(np.array(motion), kind="stable")
+    b = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, order=order)
+    r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
+    assert torch.equal(a.metrics, r.metrics)
+    assert torch.equal(a.state.x, r.state.x)
+    assert core is not None
+
+
+# -------------------------------------------------------------------- DARE
+
+
+def _dare_fixture():
+    D = np.load(os.path.join(GOLDEN, "dare_cases.npz"))
+    return D, json.loads(str(D["configs_json"]))
+
+
+def test_drop_in_controller_gains(qt):
+    from quadtrack import RiccatiLQRController
+
+    D, cfgs = _dare_fixture()
+    for i, cfg in enumerate(cfgs):
+        n = int(D["n"][i])
+        c = RiccatiLQRController(dict(cfg))
+        assert c.is_using_fallback() == bool(D["fallback"][i]), i
+        if c.is_using_fallback():
+            np.testing.assert_allclose(c.fallback_controller.K, D["K"][i][:, :6], rtol=1e-14, equal_nan=True)
+            continue
+        np.testing.assert_allclose(c.get_gain_matrix(), D["K"][i][:, :n], rtol=1e-8, atol=1e-10, err_msg=str(i))
+        np.testing.assert_allclose(c.get_riccati_solution(), D["P"][i][:n, :n], rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("structured", [True, False])
+def test_batched_dare_tuner_candidates(qt, structured):
+    """Config-4 candidates (tuner order from default_rng(42)), structured and dense kernels."""
+    from quadtrack import core
+    from quadtrack.controllers.riccati_lqr import _soa
+
+    D, cfgs = _dare_fixture()
+    idx = [i for i, c in enumerate(cfgs) if "q_pos" in c and not D["fallback"][i] and "Q" not in c]
+    dev = torch.device("cuda")
+    for n_state in (6, 9):
+        sel = [i for i in idx if int(D["n"][i]) == n_state]
+        Q = np.stack([D["Q"][i][:n_state, :n_state] for i in sel])
+        R = np.stack([D["R"][i] for i in sel])
+        mass = torch.tensor(D["mass"][sel], dtype=torch.float64, device=dev)
+        dts = set(D["dt"][sel].tolist())
+        assert dts == {0.01}
+        K, P, st, it = core.dare_batched(n_state, 0.01, 9.81, mass, _soa(Q, dev), _soa(R, dev), structured)
+        assert int(st.abs().sum()) == 0
+        assert int(it.max()) <= 40
+        Kh = K.cpu().numpy().T.reshape(-1, 4, n_state)
+        for j, i in enumerate(sel):
+            np.testing.assert_allclose(Kh[j], D["K"][i][:, :n_state], rtol=1e-8, atol=1e-10, err_msg=str(i))
+
+
+def test_dare_invalid_and_fallback(qt):
+    from quadtrack import core, solve_dare
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.controllers.riccati_lqr import build_linearized_system
+
+    A, B = build_linearized_system(0.01)
+    Q = np.diag([1e-4, 1e-4, 16, 3.6e-3, 3.6e-3, 4.0])
+    with pytest.raises(ValueError, match="positive semi-definite"):
+        solve_dare(A, B, -Q, np.eye(4))
+    with pytest.raises(ValueError, match="positive definite"):
+        solve_dare(A, B, Q, np.diag([1, 0, 1, 1.0]))
+    with pytest.raises(ValueError, match="A must be square"):
+        solve_dare(np.zeros((6, 5)), B, Q, np.eye(4))
+    P, K = solve_dare(A, B, Q, np.eye(4))
+    oP, oK = O.dare(6, A, B, Q, np.eye(4))
+    np.testing.assert_allclose(K, oK, rtol=1e-9, atol=1e-12)
+    # batched: per-episode failures fall back per episode
+    ctl = BatchedRiccatiLQR({"dt": 0.01}, q_pos=[[1e-4, 1e-4, 16], [-1.0, 1e-4, 16.0]],
+                            r_controls=[[1, 1, 1, 1], [1, 1, 1, 1]])
+    assert ctl.status.cpu().tolist() == [0, 1]
+    with pytest.raises(ValueError):
+        BatchedRiccatiLQR({"dt": 0.01, "fallback_on_failure": False}, r_controls=[[1, 1, 1, 1], [1, 0, 1, 1]])
+    assert core is not None
+
+
+def test_general_dare_random_systems(qt):
+    """solve_dare on random stabilisable systems (n up to 12, m up to 5) vs the oracle."""
+    from quadtrack import solve_dare
+
+    rng = np.random.default_rng(3)
+    for n, m in ((2, 1), (5, 2), (9, 4), (12, 5)):
+        A = rng.normal(size=(n, n)) * 0.3 + np.eye(n) * 0.5
+        B = rng.normal(size=(n, m))
+        M = rng.normal(size=(n, n))
+        Q = M @ M.T + np.eye(n) * 0.1
+        R = np.eye(m) + 0.1 * np.ones((m, m))
+        P, K = solve_dare(A, B, Q, R)
+        # residual of the DARE itself
+        BtP = B.T @ P
+        res = A.T @ P @ A - P - A.T @ P @ B @ np.linalg.solve(R + BtP @ B, BtP @ A) + Q
+        assert np.max(np.abs(res)) <= 1e-9 * max(1.0, np.max(np.abs(P)))
+        np.testing.assert_allclose(K, np.linalg.solve(R + BtP @ B, BtP @ A), rtol=1e-9, atol=1e-12)
+
+
+# ------------------------------------------------------- component kernels
+
+
+def test_target_kernel_matches_reference(qt):
+    from quadtrack.env.config import TargetParams
+    from quadtrack.env.target_motion import TargetMotion
+
+    T = np.load(os.path.join(GOLDEN, "target_states.npz"))
+    variants = json.loads(str(T["variants_json"]))
+    for vi, var in enumerate(variants):
+        for m in O.MOTIONS:
+            kw = dict(var)
+            if "center" in kw:
+                kw["center"] = tuple(kw["center"])
+            tp = TargetParams(motion_type=m, **kw)
+            for si, seed in enumerate(T["seeds"][:2]):
+                tm = TargetMotion(tp, seed=int(seed))
+                tm.reset(seed=int(seed))
+                for ti in range(0, len(T["times"]), 97):
+                    st = tm.get_state(float(T["times"][ti]))
+                    ref = T[f"v{vi}_{m}"][si, ti]
+                    np.testing.assert_allclose(st["position"], ref[0:3], rtol=1e-12, atol=1e-12)
+                    np.testing.assert_allclose(st["velocity"], ref[3:6], rtol=1e-12, atol=1e-12)
+                    np.testing.assert_allclose(st["acceleration"], ref[6:9], rtol=1e-8,
+                                               atol=1e-3 if m == "figure8" else 1e-12)
+
+
+def test_controller_kernel_sequences(qt):
+    from quadtrack import RiccatiLQRController
+
+    A = np.load(os.path.join(GOLDEN, "actions.npz"))
+    cases = json.loads(str(A["cases_json"]))
+    for ci, cfg in enumerate(cases):
+        ctl = RiccatiLQRController(dict(cfg))
+        for k, o in enumerate(A["obs"]):
+            obs = {"quadcopter": {"position": o[0:3], "velocity": o[3:6], "attitude": np.zeros(3),
+                                  "angular_velocity": np.zeros(3)},
+                   "target": {"position": o[6:9], "velocity": o[9:12], "acceleration": o[12:15]}}
+            a = ctl.compute_action(obs)
+            got = [a["thrust"], a["roll_rate"], a["pitch_rate"], a["yaw_rate"]]
+            np.testing.assert_allclose(got, A[f"case{ci}_action"][k], rtol=1e-9, atol=1e-9, err_msg=f"{ci} {k}")
+            if ctl.is_lqi_mode() and not ctl.is_using_fallback():
+                np.testing.assert_allclose(ctl.get_integral_state(), A[f"case{ci}_integral"][k], rtol=1e-12,
+                                           atol=1e-14)
+
+
+def test_lqi_known_answers(qt):
+    """test_env_dynamics.py:3745-3851 known answers through the GPU controller."""
+    from quadtrack import RiccatiLQRController
+
+    ctl = RiccatiLQRController({"dt": 0.01, "use_lqi": True, "q_int": [0.01, 0.01, 0.1], "integral_limit": 10.0})
+    obs = {"quadcopter": {"position": np.array([0.0, 0.0, 1.0]), "velocity": np.zeros(3), "attitude": np.zeros(3),
+                          "angular_velocity": np.zeros(3)},
+           "target": {"position": np.array([1.0, 0.0, 2.0]), "velocity": np.zeros(3)}}
+    ctl.compute_action(obs)
+    np.testing.assert_allclose(ctl.integral_state, [0.01, 0.0, 0.01], atol=1e-6)
+    ctl.compute_action(obs)
+    np.testing.assert_allclose(ctl.integral_state, [0.02, 0.0, 0.02], atol=1e-6)
+    ctl.reset()
+    np.testing.assert_allclose(ctl.get_integral_state(), [0, 0, 0])
+    hover = RiccatiLQRController({"dt": 0.01})
+    obs["target"]["position"] = obs["quadcopter"]["position"].copy()
+    assert hover.compute_action(obs)["thrust"] == pytest.approx(9.81, abs=0.01)
+
+
+def test_open_loop_step_kernel(qt):
+    from quadtrack import QuadcopterEnv
+
+    OL = np.load(os.path.join(GOLDEN, "open_loop.npz"))
+    cases = json.loads(str(OL["cases_json"]))
+    for ci, case in enumerate(cases):
+        cfg = json.loads(json.dumps(case["env"]))
+        cfg.setdefault("target", {})["motion_type"] = case["motion"]
+        cfg["logging"] = {"enabled": False}
+        env = QuadcopterEnv(cfg)
+        env.reset(seed=case["seed"])
+        X, info = OL[f"case{ci}_states"], OL[f"case{ci}_info"]
+        np.testing.assert_allclose(env.get_state_vector(), X[0], atol=1e-15)
+        for k in range(len(OL["actions"])):
+            if np.isnan(info[k, 0]):
+                break
+            _, r, done, inf = env.step(OL["actions"][k].copy())
+            np.testing.assert_allclose(env.get_state_vector(), X[k + 1], rtol=1e-9, atol=1e-9, err_msg=f"{ci} {k}")
+            assert inf["tracking_error"] == pytest.approx(info[k, 0], rel=1e-9, abs=1e-9)
+            assert inf["on_target_ratio"] == pytest.approx(info[k, 1])
+            assert inf["action_violations"] == int(info[k, 2])
+            assert done == bool(info[k, 3])
+            assert inf["time"] == info[k, 5]
+
+
+# ----------------------------------------------------------------- metrics
+
+
+def test_metric_helpers_known_answers(qt):
+    """Hand-computed answers of the reference's TestMetrics (tests/test_eval.py:23-148)."""
+    from quadtrack.utils import metrics as M
+
+    e = M.compute_tracking_error(np.array([[0, 0, 0], [1, 0, 0], [2, 0, 0]]), np.zeros((3, 3)))
+    np.testing.assert_allclose(e, [0, 1, 2])
+    assert M.compute_tracking_error(np.array([[1, 1, 1]]), np.zeros((1, 3)))[0] == pytest.approx(np.sqrt(3))
+    with pytest.raises(ValueError):
+        M.compute_tracking_error(np.zeros((1, 3)), np.zeros((2, 3)))
+    assert M.compute_on_target_ratio(np.array([0.1, 0.2, 0.3, 0.4]), 0.5) == 1.0
+    assert M.compute_on_target_ratio(np.array([0.6, 0.7, 0.8]), 0.5) == 0.0
+    assert M.compute_on_target_ratio(np.array([0.1, 0.6, 0.2, 0.7]), 0.5) == 0.5
+    assert M.compute_on_target_ratio(np.array([]), 0.5) == 0.0
+    tot, mean = M.compute_control_effort(np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0]]))
+    assert tot == pytest.approx(3.0) and mean == pytest.approx(1.0)
+    assert M.compute_control_effort(np.array([])) == (0.0, 0.0)
+    assert M.detect_overshoots(np.array([0.1] * 20), 0.5) == (0, 0.0)
+    errs = np.array([0.1] * 5 + [0.8] * 12 + [0.1] * 5)
+    cnt, mx = M.detect_overshoots(errs, 0.5, window_size=10)
+    assert cnt == 1 and mx == pytest.approx(0.3)
+    assert M.detect_overshoots(np.array([0.1, 0.8]), 0.5) == (0, 0.0)
+
+
+def test_episode_metrics_and_summary(qt):
+    from quadtrack.utils import metrics as M
+
+    rng = np.random.default_rng(0)
+    eps = []
+    for _ in range(7):
+        S = int(rng.integers(5, 50))
+        data = [{"time": 0.01 * (k + 1), "quadcopter_position": rng.normal(size=3).tolist(),
+                 "target_position": rng.normal(size=3).tolist(), "action": rng.normal(size=4).tolist()}
+                for k in range(S)]
+        m = M.compute_episode_metrics(data, M.SuccessCriteria(min_episode_duration=0.1, target_radius=1.5))
+        qp = np.array([d["quadcopter_position"] for d in data])
+        tp = np.array([d["target_position"] for d in data])
+        err = np.linalg.norm(tp - qp, axis=1)
+        assert m.mean_tracking_error == pytest.approx(err.mean(), rel=1e-12)
+        assert m.rms_tracking_error == pytest.approx(np.sqrt((err ** 2).mean()), rel=1e-12)
+        assert m.max_tracking_error == err.max()
+        assert m.on_target_ratio == pytest.approx((err <= 1.5).mean())
+        eps.append(m)
+    s = M.compute_evaluation_summary(eps)
+    r = np.array([m.on_target_ratio for m in eps])
+    er = np.array([m.mean_tracking_error for m in eps])
+    assert s.mean_on_target_ratio == pytest.approx(r.mean(), rel=1e-12)
+    assert s.std_on_target_ratio == pytest.approx(r.std(), rel=1e-9, abs=1e-15)
+    assert s.std_tracking_error == pytest.approx(er.std(), rel=1e-9)
+    assert s.best_episode_idx == int(np.argmax(r)) and s.worst_episode_idx == int(np.argmin(r))
+    assert "EVALUATION SUMMARY" in M.format_metrics_report(s)
+    assert M.compute_episode_metrics([]).termination_reason == "no_data"
+
+
+def test_evaluate_batched_vs_evaluator(qt):
+    """Batched evaluator == the drop-in sequential Evaluator for LQR (no
+    integral, so the carry-over of SURVEY F8 is moot)."""
+    from quadtrack import Evaluator, RiccatiLQRController, evaluate_batched
+    from quadtrack.env import EnvConfig
+
+    cfg = EnvConfig.from_dict({"target": {"motion_type": "circular"}, "simulation": {"max_episode_time": 3.0},
+                               "logging": {"enabled": False}})
+    ctl = RiccatiLQRController({"dt": 0.01})
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        seq = Evaluator(ctl, cfg, output_dir=d).evaluate(num_episodes=3, base_seed=42, verbose=False)
+    bat = evaluate_batched(ctl, cfg, num_episodes=3, base_seed=42)
+    for k in ("mean_on_target_ratio", "mean_tracking_error", "std_tracking_error", "mean_control_effort"):
+        assert getattr(bat, k) == pytest.approx(getattr(seq, k), rel=1e-9, abs=1e-12), k
+    assert bat.best_episode_idx == seq.best_episode_idx
