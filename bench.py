@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--episodes", type=int, default=65536, help="episodes per GPU")
     ap.add_argument("--motion", default="linear")
-    ap.add_argument("--cpu-sample", type=int, default=8192, help="episodes in the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=65536, help="episodes in the CPU baseline sample (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()

@@ -143,6 +143,10 @@ typedef struct qt_batch {
   const double* K;              /* gains, layout above */
   int32_t k_cols;               /* 6 (LQR) or 9 (LQI) */
   int32_t k_per_episode;        /* 0: one shared K (m = 1), 1: m = n */
+  int32_t k_structured;         /* 1: the caller asserts every K entry outside the per-axis
+                                   pattern (z->thrust, y->roll, x->pitch) is exactly 0, as the
+                                   diagonal-weight DARE produces; the kernel then skips them */
+  int32_t pad_;
   const int32_t* order;         /* [n] or NULL */
 } qt_batch;
 

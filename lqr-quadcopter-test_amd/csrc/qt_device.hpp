@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "../../include/quadtrack.h"
+#include "qt_math.hpp"
 
 namespace qt {
 
@@ -27,17 +28,6 @@ __device__ __forceinline__ double clipd(double v, double lo, double hi) {
 }
 
 __device__ __forceinline__ double norm3(double a, double b, double c) { return sqrt(a * a + b * b + c * c); }
-
-// numpy float remainder: floor-mod, sign of the divisor (quadcopter_env.py:457)
-__device__ __forceinline__ double py_mod(double a, double b) {
-  double m = fmod(a, b);
-  if (m != 0.0) {
-    if ((b < 0) != (m < 0)) m += b;
-  } else {
-    m = copysign(0.0, b);
-  }
-  return m;
-}
 
 // np.sign equality used by the LQI anti-windup (riccati_lqr.py:881-883):
 // sign(NaN) is NaN, which equals nothing.
@@ -109,7 +99,7 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
   } else if (motion == QT_MOTION_CIRCULAR) {
     double ang = pt.c0 + pt.c1 * t;
     double s, c;
-    sincos(ang, &s, &c);
+    fast_sincos(ang, &s, &c);
     const double r = e.radius, om = pt.c1;
     o.p[0] = e.center[0] + r * c;
     o.p[1] = e.center[1] + r * s;
@@ -126,7 +116,7 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       double s, c;
-      sincos(om[i] * t + ph[i], &s, &c);
+      fast_sincos(om[i] * t + ph[i], &s, &c);
       o.p[i] = e.center[i] + amp[i] * s;
       o.v[i] = amp[i] * om[i] * c;
       if (WANT_ACC) o.a[i] = -amp[i] * (om[i] * om[i]) * s;
@@ -134,7 +124,7 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
   } else if (motion == QT_MOTION_FIGURE8) {
     const double sc = e.amplitude, om = pt.o0;
     double st, ct;
-    sincos(om * t, &st, &ct);
+    fast_sincos(om * t, &st, &ct);
     double den = 1.0 + st * st;
     o.p[0] = e.center[0] + sc * ct / den;
     o.p[1] = e.center[1] + sc * st * ct / den;
@@ -147,7 +137,7 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;
       double stp, ctp;
-      sincos(om * (t + h), &stp, &ctp);
+      fast_sincos(om * (t + h), &stp, &ctp);
       double denp = 1.0 + stp * stp;
       double pp0 = e.center[0] + sc * ctp / denp;
       double pp1 = e.center[1] + sc * stp * ctp / denp;
@@ -183,9 +173,9 @@ __device__ __forceinline__ Plant make_plant(const qt_env_params& e, double mass)
 __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant& pl, const double* s,
                                             const double* u, double* d) {
   double sphi, cphi, sth, cth, spsi, cpsi;
-  sincos(s[6], &sphi, &cphi);
-  sincos(s[7], &sth, &cth);
-  sincos(s[8], &spsi, &cpsi);
+  fast_sincos(s[6], &sphi, &cphi);
+  fast_sincos(s[7], &sth, &cth);
+  fast_sincos(s[8], &spsi, &cpsi);
   const double T = u[0];
   const double tw0 = (cpsi * sth * cphi + spsi * sphi) * T;
   const double tw1 = (spsi * sth * cphi - cpsi * sphi) * T;
@@ -249,7 +239,7 @@ __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
 #pragma unroll
   for (int i = 9; i < 12; ++i) x[i] = clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity);
 #pragma unroll
-  for (int i = 6; i < 9; ++i) x[i] = py_mod(x[i] + kPi, kTwoPi) - kPi;
+  for (int i = 6; i < 9; ++i) x[i] = py_mod_2pi(x[i] + kPi, kTwoPi) - kPi;
   x[6] = clipd(x[6], -kMaxTilt, kMaxTilt);
   x[7] = clipd(x[7], -kMaxTilt, kMaxTilt);
 }
@@ -292,17 +282,33 @@ __device__ __forceinline__ int termination(const qt_env_params& e, double t, con
 
 // ------------------------------------------------------------ controller
 
-// Gains as seen by one lane: 4 x KC, loaded once per launch.
-template <int KC>
+// Gains as seen by one lane, loaded once per launch.  Dense: the full 4 x KC
+// matrix.  Structured (KS): only the per-axis entries — K[0][2], K[0][5],
+// K[1][1], K[1][4], K[2][0], K[2][3] (+ K[0][8], K[1][7], K[2][6] for LQI) —
+// for gains whose every other entry is exactly zero (the per-axis DARE with
+// diagonal Q/R, riccati_lqr.py:602-700).  With finite errors (a running
+// episode) adding those exact zeros changes nothing, so both forms agree bit
+// for bit.
+template <int KC, bool KS>
 struct Gains {
-  double k[4 * KC];
+  static constexpr int kCount = KS ? (KC == 9 ? 9 : 6) : 4 * KC;
+  double k[kCount];
 };
+
+// element index (row-major r*KC + c) of structured slot j
+template <int KC>
+__host__ __device__ constexpr int structured_index(int j) {
+  // (row, col): (0,2) (0,5) (1,1) (1,4) (2,0) (2,3) [(0,8) (1,7) (2,6)]
+  constexpr int rows[9] = {0, 0, 1, 1, 2, 2, 0, 1, 2};
+  constexpr int cols[9] = {2, 5, 1, 4, 0, 3, 8, 7, 6};
+  return rows[j] * KC + cols[j];
+}
 
 // RiccatiLQRController.compute_action (riccati_lqr.py:779-967) given the
 // observation the env returned (quad p, v; target p, v, a).  LQI integral
 // update 869-900, output clamps 907-921.  Returns true when saturated.
-template <int KC, bool FF>
-__device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC>& G, double hover,
+template <int KC, bool FF, bool KS>
+__device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC, KS>& G, double hover,
                                                const double* qp, const double* qv, const Target& tg,
                                                double* integ, double* u, double* diag = nullptr) {
   double ep[3], ev[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
@@ -348,15 +354,27 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
 #pragma unroll
       for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i], -lim, lim);
     }
+    if (KS) {
+      uf[0] = (G.k[0] * s[2] + G.k[1] * s[5]) + G.k[6] * integ[2];
+      uf[1] = (G.k[2] * s[1] + G.k[3] * s[4]) + G.k[7] * integ[1];
+      uf[2] = (G.k[4] * s[0] + G.k[5] * s[3]) + G.k[8] * integ[0];
+      uf[3] = 0.0;
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double a = 0.0, b = 0.0;
+      for (int r = 0; r < 4; ++r) {
+        double a = 0.0, b = 0.0;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) a += G.k[r * KC + j] * s[j];
+        for (int j = 0; j < 6; ++j) a += G.k[r * KC + j] * s[j];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) b += G.k[r * KC + 6 + j] * integ[j];
-      uf[r] = a + b;
+        for (int j = 0; j < 3; ++j) b += G.k[r * KC + 6 + j] * integ[j];
+        uf[r] = a + b;
+      }
     }
+  } else if (KS) {
+    uf[0] = G.k[0] * s[2] + G.k[1] * s[5];
+    uf[1] = G.k[2] * s[1] + G.k[3] * s[4];
+    uf[2] = G.k[4] * s[0] + G.k[5] * s[3];
+    uf[3] = 0.0;
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

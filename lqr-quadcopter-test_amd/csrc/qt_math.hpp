@@ -1,0 +1,83 @@
+// qt_math.hpp — FP64 elementary functions for the closed-loop kernels.
+//
+// The library sin/cos carry a Payne-Hanek path for huge arguments that costs
+// registers and branches in every call; on this path every argument is small
+// (attitude angles are wrapped to [-pi, pi] each step and move <= 0.11 rad
+// inside an RK4 step; target phases stay below ~2e3 rad), so a Cody-Waite
+// reduction by pi/2 with a 3-part constant and the classic minimax kernels on
+// [-pi/4, pi/4] give <= ~1 ulp results in ~30 straight-line operations.
+//
+// Plain C++ so that the same header builds for the host (tests/test_math.py
+// checks it against numpy) and for gfx950.
+#pragma once
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define QT_HD __host__ __device__ __forceinline__
+#else
+#include <cmath>
+#define QT_HD inline
+#endif
+
+namespace qt {
+
+// pi/2 = P1 + P2 + P3 (each the double nearest the remaining tail)
+constexpr double kPio2_1 = 1.5707963267948966;
+constexpr double kPio2_2 = 6.123233995736766e-17;
+constexpr double kPio2_3 = -1.4973849048591698e-33;
+constexpr double kTwoOverPi = 0.6366197723675814;
+
+// minimax polynomials on [-pi/4, pi/4] (the fdlibm kernel coefficients)
+constexpr double kS1 = -1.66666666666666324348e-01, kS2 = 8.33333333332248946124e-03,
+                 kS3 = -1.98412698298579493134e-04, kS4 = 2.75573137070700676789e-06,
+                 kS5 = -2.50507602534068634195e-08, kS6 = 1.58969099521155010221e-10;
+constexpr double kC1 = 4.16666666666666019037e-02, kC2 = -1.38888888888741095749e-03,
+                 kC3 = 2.48015872894767294178e-05, kC4 = -2.75573143513906633035e-07,
+                 kC5 = 2.08757232129817482790e-09, kC6 = -1.13596475577881948265e-11;
+
+QT_HD void sincos_kernel(double r, double* s, double* c) {
+  const double z = r * r;
+  const double v = z * r;
+  const double ps = kS2 + z * (kS3 + z * (kS4 + z * (kS5 + z * kS6)));
+  *s = r + v * (kS1 + z * ps);
+  const double pc = z * (kC1 + z * (kC2 + z * (kC3 + z * (kC4 + z * (kC5 + z * kC6)))));
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  *c = w + (((1.0 - w) - hz) + z * pc);
+}
+
+// sin and cos of x.  Accurate (<= ~1 ulp) for |x| < 2^40; NaN and Inf give
+// NaN.  Domain on this path: |x| < 2e3 (see the header comment).
+QT_HD void fast_sincos(double x, double* s, double* c) {
+  const double k = rint(x * kTwoOverPi);
+  double r = fma(-k, kPio2_1, x);
+  r = fma(-k, kPio2_2, r);
+  r = fma(-k, kPio2_3, r);
+  double sr, cr;
+  sincos_kernel(r, &sr, &cr);
+  const int q = static_cast<int>(k) & 3;
+  const double s01 = (q & 1) ? cr : sr;
+  const double c01 = (q & 1) ? -sr : cr;
+  *s = (q & 2) ? -s01 : s01;
+  *c = (q & 2) ? -c01 : c01;
+}
+
+// numpy's float remainder: (a % b) with the sign of b, b = 2*pi here
+// (quadcopter_env.py:457).  For |a| < 4*pi the single subtraction / addition
+// is exact (Sterbenz), so it equals fmod bit for bit; larger |a| use fmod.
+QT_HD double py_mod_2pi(double a, double two_pi) {
+  double m;
+  if (fabs(a) < 2.0 * two_pi) {
+    m = a >= two_pi ? a - two_pi : (a <= -two_pi ? a + two_pi : a);
+  } else {
+    m = fmod(a, two_pi);
+  }
+  if (m != 0.0) {
+    if (m < 0) m += two_pi;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
+
+}  // namespace qt

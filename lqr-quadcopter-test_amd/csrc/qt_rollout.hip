@@ -86,14 +86,14 @@ __device__ __forceinline__ Pattern pattern_of(const BatchDev& b, const qt_env_pa
   return make_pattern(e, motion, r0, r1, r2);
 }
 
-template <int KC>
-__device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<KC>& G) {
-  if (b.k_per_episode) {
+template <int KC, bool KS>
+__device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<KC, KS>& G) {
+  const int64_t m = b.k_per_episode ? b.n : 1;
+  const int64_t col = b.k_per_episode ? ep : 0;  // shared: uniform address -> scalar loads
 #pragma unroll
-    for (int j = 0; j < 4 * KC; ++j) G.k[j] = b.K[(int64_t)j * b.n + ep];
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4 * KC; ++j) G.k[j] = b.K[j];  // uniform address: scalar loads
+  for (int j = 0; j < Gains<KC, KS>::kCount; ++j) {
+    const int idx = KS ? structured_index<KC>(j) : j;
+    G.k[j] = b.K[(int64_t)idx * m + col];
   }
 }
 
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev
 // ---------------------------------------------------------------- rollout
 
 // MOTION >= 0 specialises the target pattern; -1 reads it per episode.
-template <int MOTION, int KC, bool FF>
+template <int MOTION, int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec) {
@@ -164,8 +164,8 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   const Pattern pt = pattern_of(b, e, motion, ep);
   const Plant pl = make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
   const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
-  Gains<KC> G;
-  load_gains<KC>(b, ep, G);
+  Gains<KC, KS> G;
+  load_gains<KC, KS>(b, ep, G);
 
   double x[12], integ[3] = {0, 0, 0};
 #pragma unroll
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
     double u[4];
-    compute_action<KC, FF>(c, G, hover, x, x + 3, tg, integ, u);
+    compute_action<KC, FF, KS>(c, G, hover, x, x + 3, tg, integ, u);
     // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
     const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
     const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
@@ -295,8 +295,8 @@ __global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchD
   const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (slot >= b.n) return;
   const int64_t n = b.n, ep = episode_of(b, slot);
-  Gains<KC> G;
-  load_gains<KC>(b, ep, G);
+  Gains<KC, false> G;
+  load_gains<KC, false>(b, ep, G);
   double qp[3], qv[3], in[3] = {0, 0, 0}, u[4];
   Target tg;
 #pragma unroll
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchD
   }
   const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
   double dg[16];
-  const bool sat = compute_action<KC, true>(c, G, hover, qp, qv, tg, in, u, dg);
+  const bool sat = compute_action<KC, true, false>(c, G, hover, qp, qv, tg, in, u, dg);
 #pragma unroll
   for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
   if (diag) {
@@ -514,27 +514,44 @@ int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
 
 int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
 
-template <int KC, bool FF>
+template <int KC, bool FF, bool KS>
 void launch_rollout_motion(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                            const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
   switch (motion) {
     case QT_MOTION_STATIONARY:
-      rollout_kernel<QT_MOTION_STATIONARY, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<QT_MOTION_STATIONARY, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_LINEAR:
-      rollout_kernel<QT_MOTION_LINEAR, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<QT_MOTION_LINEAR, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_CIRCULAR:
-      rollout_kernel<QT_MOTION_CIRCULAR, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<QT_MOTION_CIRCULAR, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_SINUSOIDAL:
-      rollout_kernel<QT_MOTION_SINUSOIDAL, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<QT_MOTION_SINUSOIDAL, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_FIGURE8:
-      rollout_kernel<QT_MOTION_FIGURE8, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<QT_MOTION_FIGURE8, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
       break;
     default:
-      rollout_kernel<-1, KC, FF><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      rollout_kernel<-1, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+  }
+}
+
+template <int KC>
+void launch_rollout(bool ff, bool ks, int motion, int grid, hipStream_t s, const qt_env_params& e,
+                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
+                    double* rec) {
+  if (ff) {
+    if (ks)
+      launch_rollout_motion<KC, true, true>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+    else
+      launch_rollout_motion<KC, true, false>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+  } else {
+    if (ks)
+      launch_rollout_motion<KC, false, true>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+    else
+      launch_rollout_motion<KC, false, false>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
   }
 }
 
@@ -566,17 +583,11 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   const int motion = batch->motion ? -1 : env->motion;
   hipStream_t s = (hipStream_t)stream;
   const bool ff = ctrl->feedforward_enabled != 0;
-  if (batch->k_cols == 9) {
-    if (ff)
-      launch_rollout_motion<9, true>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-    else
-      launch_rollout_motion<9, false>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-  } else {
-    if (ff)
-      launch_rollout_motion<6, true>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-    else
-      launch_rollout_motion<6, false>(motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-  }
+  const bool ks = batch->k_structured != 0;
+  if (batch->k_cols == 9)
+    launch_rollout<9>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+  else
+    launch_rollout<6>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   return check_launch();
 }
 

@@ -67,7 +67,8 @@ class Batch(C.Structure):
 
     _fields_ = [("n", C.c_int64), ("motion", C.c_void_p), ("pattern", C.c_void_p), ("plant_mass", C.c_void_p),
                 ("hover_thrust", C.c_void_p), ("K", C.c_void_p), ("k_cols", C.c_int32),
-                ("k_per_episode", C.c_int32), ("order", C.c_void_p)]
+                ("k_per_episode", C.c_int32), ("k_structured", C.c_int32), ("pad_", C.c_int32),
+                ("order", C.c_void_p)]
 
 
 class State(C.Structure):

@@ -463,6 +463,7 @@ class BatchedRiccatiLQR:
         self.mass = torch.as_tensor(masses, device=dev)
         self.K, self.P, self.status, self.iters = core.dare_batched(
             self.n_state, self.dt, self.gravity, self.mass, _soa(Qm, dev), _soa(Rm, dev), structured)
+        self.k_structured = core.gains_structured(self.K, self.k_cols)
         self.fallback_on_failure = config.get("fallback_on_failure", True)
         bad = self.status != DARE_OK
         if bool(bad.any()):

@@ -39,6 +39,7 @@ class EpisodeBatch:
     plant_mass: torch.Tensor | None = None    # [n]
     hover: torch.Tensor | None = None         # [n]
     order: torch.Tensor | None = None         # [n] int32
+    k_structured: bool = False                # every off-axis K entry is exactly zero
 
     def c_batch(self, with_k=True) -> Batch:
         b = Batch()
@@ -50,6 +51,7 @@ class EpisodeBatch:
         b.K = ptr(self.K) if with_k else None
         b.k_cols = self.k_cols
         b.k_per_episode = int(self.K.shape[1] != 1)
+        b.k_structured = int(self.k_structured)
         b.order = ptr(self.order)
         return b
 
@@ -73,6 +75,19 @@ class RolloutState:
         s = State()
         s.x, s.integ, s.t, s.acc, s.target = (ptr(v) for v in (self.x, self.integ, self.t, self.acc, self.target))
         return s
+
+
+_AXIS_PATTERN = {6: [(0, 2), (0, 5), (1, 1), (1, 4), (2, 0), (2, 3)]}
+_AXIS_PATTERN[9] = _AXIS_PATTERN[6] + [(0, 8), (1, 7), (2, 6)]
+
+
+def gains_structured(K: torch.Tensor, k_cols: int) -> bool:
+    """True when every entry of K ([4*k_cols, m]) outside the per-axis pattern
+    is exactly zero (qt_batch.k_structured)."""
+    mask = torch.ones(4 * k_cols, dtype=torch.bool, device=K.device)
+    for r, c in _AXIS_PATTERN[k_cols]:
+        mask[r * k_cols + c] = False
+    return bool((K[mask] == 0).all().item())
 
 
 def to_device(a, device, dtype=F64) -> torch.Tensor:
