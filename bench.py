@@ -163,6 +163,10 @@ def main():
 
     if rank == 0:
         achieved = FLOPS_PER_ENV_STEP * local_env_steps / (kern_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic("rollout_kernel<1, 6, false, true>")
+        # algorithmic HBM bytes of one launch: per-episode state in (x 12, target 9, t, acc 14,
+        # pattern 3 doubles) and out (x, target, t, acc); gains are a broadcast
+        algo_bytes = (39 + 36) * 8 * n
         line = {
             "metric": "env-steps/sec at 65 536 parallel episodes per GPU (30 s @ dt=0.01, Riccati-LQR closed loop)",
             "value": round(value, 1),
@@ -181,8 +185,11 @@ def main():
                                    f"target, Riccati-LQR shared K, RK4 dt=0.01",
                        "episodes_per_gpu": n, "episodes_total": n * world, "parallelism": f"episode-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "rollout_kernel<LINEAR,6,false>", "kernel_ms": round(kern_ms, 4),
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": algo_bytes,
+                         "hbm_GBps_achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3),
+                         "kernel": "rollout_kernel<LINEAR, K=6, no-FF, structured K>", "kernel_ms": round(kern_ms, 4),
                          "flops_per_env_step": FLOPS_PER_ENV_STEP},
             "cpu_baseline": cpu,
             "tracking": track,
@@ -191,6 +198,32 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel_tag: str):
+    """HBM bytes per rollout launch from the committed rocprofv3 PMC passes
+    (profiles/r*/pmc_FETCH_SIZE.csv, pmc_WRITE_SIZE.csv; scripts/profile_session.sh).
+    gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
+    (MI355X_MICROARCH.md §HBM), so it is doubled; both counters are in KiB."""
+    import csv
+    import glob
+
+    dirs = sorted(d for d in glob.glob(os.path.join(ROOT, "profiles", "r*"))
+                  if os.path.exists(os.path.join(d, "pmc_FETCH_SIZE.csv")))
+    if not dirs:
+        return None, None
+
+    def avg(path, counter):
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                if r["Counter_Name"] == counter and kernel_tag in r["Kernel_Name"]]
+        return sum(vals) / len(vals) if vals else None
+
+    d = dirs[-1]
+    f = avg(os.path.join(d, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
+    w = avg(os.path.join(d, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
+    if f is None or w is None:
+        return None, d
+    return (2.0 * f + w) * 1024.0, os.path.relpath(d, ROOT)
 
 
 def cpu_baseline(args, cfg, seeds, gpu_met):
