@@ -170,12 +170,39 @@ __device__ __forceinline__ Plant make_plant(const qt_env_params& e, double mass)
 // the ZYX rotation matrix multiplies the body thrust [0,0,T] (393).  Divisions
 // by mass and by the 0.1 s rate time constant are taken as multiplications by
 // reciprocals (<= 1 ulp per term; the closed loop is not chaotic).
+// sin / cos of the three attitude angles of a stage state
+struct Trig {
+  double s[3], c[3];
+};
+
+__device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) fast_sincos(ang[i], &t.s[i], &t.c[i]);
+}
+
+// Trig of the RK4 stage angles  ang_i + delta_i  from the trig of ang_i:
+// sin(a + d) = sin a cos d + cos a sin d,  cos(a + d) = cos a cos d - sin a sin d,
+// with sin d / cos d from small_sincos.  The stage offsets are h * (body rate)
+// <= dt * ~12 rad/s; an offset beyond the polynomial's range takes fast_sincos.
+__device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t) {
+  const double dm = fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
+  if (dm <= kSmallAngle) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double sd, cd;
+      small_sincos(delta[i], &sd, &cd);
+      t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
+      t.c[i] = fma(t0.c[i], cd, -(t0.s[i] * sd));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) fast_sincos(ang[i] + delta[i], &t.s[i], &t.c[i]);
+  }
+}
+
 __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant& pl, const double* s,
-                                            const double* u, double* d) {
-  double sphi, cphi, sth, cth, spsi, cpsi;
-  fast_sincos(s[6], &sphi, &cphi);
-  fast_sincos(s[7], &sth, &cth);
-  fast_sincos(s[8], &spsi, &cpsi);
+                                            const double* u, const Trig& tr, double* d) {
+  const double sphi = tr.s[0], cphi = tr.c[0], sth = tr.s[1], cth = tr.c[1], spsi = tr.s[2], cpsi = tr.c[2];
   const double T = u[0];
   const double tw0 = (cpsi * sth * cphi + spsi * sphi) * T;
   const double tw1 = (spsi * sth * cphi - cpsi * sphi) * T;
@@ -198,32 +225,46 @@ __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant&
 __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
   const double dt = e.dt;
   double k[12];
-  derivatives(e, pl, x, u, k);
+  Trig t0, ts;
+  trig_of(x + 6, t0);
+  derivatives(e, pl, x, u, t0, k);
   if (e.integrator == 1) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
     return;
   }
-  double acc[12], tmp[12];
+  // Stage states.  Their angles only enter through sin/cos (derivatives of
+  // the angles are the body rates), so stage trig is the step-start trig
+  // shifted by the stage offset h * k[6..8].
+  double acc[12], tmp[12], del[3];
   const double h2 = 0.5 * dt;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     acc[i] = k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
-  derivatives(e, pl, tmp, u, k);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
-  derivatives(e, pl, tmp, u, k);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + dt * k[i];
   }
-  derivatives(e, pl, tmp, u, k);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) del[i] = dt * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
   const double h6 = dt / 6.0;
 #pragma unroll
   for (int i = 0; i < 12; ++i) x[i] = x[i] + h6 * (acc[i] + k[i]);

@@ -26,9 +26,13 @@ int main(int argc, char** argv) {
     double s, c;
     qt::fast_sincos(a, &s, &c);
     double m = qt::py_mod_2pi(a, 6.283185307179586);
+    double ss, cs;
+    qt::small_sincos(a, &ss, &cs);
     fwrite(&s, 8, 1, o);
     fwrite(&c, 8, 1, o);
     fwrite(&m, 8, 1, o);
+    fwrite(&ss, 8, 1, o);
+    fwrite(&cs, 8, 1, o);
   }
   fclose(o);
   return 0;
@@ -48,7 +52,7 @@ def probe(tmp_path_factory):
         x = np.ascontiguousarray(x, dtype=np.float64)
         (d / "in.bin").write_bytes(x.tobytes())
         subprocess.run([str(exe), str(d / "in.bin"), str(d / "out.bin")], check=True)
-        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 3)
+        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 5)
 
     return run
 
@@ -76,6 +80,23 @@ def test_sincos_accuracy(probe):
     small = np.abs(x) <= np.pi + 0.2
     assert np.max(ulp_err(s[small], np.sin(x[small]))[np.abs(np.sin(x[small])) > 1e-3]) <= 2.0
     assert np.max(ulp_err(c[small], np.cos(x[small]))[np.abs(np.cos(x[small])) > 1e-3]) <= 2.0
+
+
+def test_small_angle_sincos_and_rotation(probe):
+    """The RK4 stage trig: small_sincos on |d| <= 0.25 and the angle-addition
+    rotation used for stages 2-4 (qt_device.hpp trig_shift)."""
+    rng = np.random.default_rng(2)
+    d = np.concatenate([rng.uniform(-0.25, 0.25, 200000), [0.0, -0.0, 1e-12, 0.25, -0.25]])
+    out = probe(d)
+    ss, cs = out[:, 3], out[:, 4]
+    assert np.max(ulp_err(ss, np.sin(d))[np.abs(d) > 1e-300]) <= 1.0
+    assert np.max(ulp_err(cs, np.cos(d))) <= 1.0
+    a = rng.uniform(-np.pi, np.pi, d.size)
+    base = probe(a)
+    s = np.fma(base[:, 0], cs, base[:, 1] * ss) if hasattr(np, "fma") else base[:, 0] * cs + base[:, 1] * ss
+    c = base[:, 1] * cs - base[:, 0] * ss
+    assert np.max(np.abs(s - np.sin(a + d))) <= 4.5e-16
+    assert np.max(np.abs(c - np.cos(a + d))) <= 4.5e-16
 
 
 def test_sincos_nonfinite(probe):
