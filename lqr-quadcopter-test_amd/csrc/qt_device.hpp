@@ -270,51 +270,87 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   for (int i = 0; i < 12; ++i) x[i] = x[i] + h6 * (acc[i] + k[i]);
 }
 
-// _apply_state_constraints (quadcopter_env.py:428-465)
+// Clip of a value known to be a number: one v_max + one v_min.  (IEEE maxNum
+// would turn a NaN into a bound, which np.clip does not; callers use it only
+// where NaN cannot reach or check for it separately.)
+__device__ __forceinline__ double clip_num(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
+
+// `sqrt(s) > r` for s = a sum of squares and r >= 0, without the square root
+// unless s lies within 1e-14 of r^2 (sqrt is correctly rounded and monotone,
+// so outside that band the squared comparison decides it identically).
+__device__ __forceinline__ bool norm_gt(double s, double r) {
+  const double r2 = r * r;
+  if (s > r2 * (1.0 + 1e-14)) return true;
+  if (!(s >= r2 * (1.0 - 1e-14))) return false;  // also NaN -> false, like NaN > r
+  return sqrt(s) > r;
+}
+
+// `sqrt(s) <= r` likewise (NaN -> false).
+__device__ __forceinline__ bool norm_le(double s, double r) {
+  const double r2 = r * r;
+  if (s < r2 * (1.0 - 1e-14)) return true;
+  if (s > r2 * (1.0 + 1e-14)) return false;
+  return sqrt(s) <= r;
+}
+
+// _apply_state_constraints (quadcopter_env.py:428-465).  EXACT_NAN keeps
+// np.clip's NaN propagation for the rate / tilt clips (open-loop step on
+// caller-supplied states); inside the fused rollout the state is finite by
+// construction (finite reset, finite clipped actions, bounded updates).
+template <bool EXACT_NAN = true>
 __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
-  double vm = norm3(x[3], x[4], x[5]);
-  if (vm > e.max_velocity) {
+  const double s = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
+  if (norm_gt(s, e.max_velocity)) {
+    const double vm = sqrt(s);
 #pragma unroll
     for (int i = 3; i < 6; ++i) x[i] = x[i] / vm * e.max_velocity;
   }
 #pragma unroll
-  for (int i = 9; i < 12; ++i) x[i] = clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+  for (int i = 9; i < 12; ++i)
+    x[i] = EXACT_NAN ? clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity)
+                     : clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
 #pragma unroll
   for (int i = 6; i < 9; ++i) x[i] = py_mod_2pi(x[i] + kPi, kTwoPi) - kPi;
-  x[6] = clipd(x[6], -kMaxTilt, kMaxTilt);
-  x[7] = clipd(x[7], -kMaxTilt, kMaxTilt);
+  x[6] = EXACT_NAN ? clipd(x[6], -kMaxTilt, kMaxTilt) : clip_num(x[6], -kMaxTilt, kMaxTilt);
+  x[7] = EXACT_NAN ? clipd(x[7], -kMaxTilt, kMaxTilt) : clip_num(x[7], -kMaxTilt, kMaxTilt);
 }
 
 // _parse_and_validate_action (quadcopter_env.py:234-293) on an array action;
-// returns true when any violation was recorded.
+// returns true when any violation was recorded.  A finite 4-sum proves every
+// component finite; otherwise the per-component NaN/Inf zeroing runs.
 __device__ __forceinline__ bool parse_action(const qt_env_params& e, const double* in, double* a) {
   bool viol = false;
-  bool finite = isfinite(in[0]) && isfinite(in[1]) && isfinite(in[2]) && isfinite(in[3]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) a[i] = (finite || isfinite(in[i])) ? in[i] : 0.0;
-  viol = !finite;
-  if (a[0] < e.min_thrust) {
-    viol = true;
-    a[0] = e.min_thrust;
-  } else if (a[0] > e.max_thrust) {
-    viol = true;
-    a[0] = e.max_thrust;
+  for (int i = 0; i < 4; ++i) a[i] = in[i];
+  if (!isfinite((in[0] + in[1]) + (in[2] + in[3]))) {
+    const bool finite = isfinite(in[0]) && isfinite(in[1]) && isfinite(in[2]) && isfinite(in[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = isfinite(in[i]) ? in[i] : 0.0;
+    viol = !finite;
   }
+  // thrust: min if below, else max if above; rates: clip when |r| > max
+  const double t = a[0] < e.min_thrust ? e.min_thrust : fmin(a[0], e.max_thrust);
+  viol = viol || (t != a[0]);
+  a[0] = t;
 #pragma unroll
   for (int i = 1; i < 4; ++i) {
-    if (fabs(a[i]) > e.max_angular_rate) {
-      viol = true;
-      a[i] = clipd(a[i], -e.max_angular_rate, e.max_angular_rate);
-    }
+    const double r = clip_num(a[i], -e.max_angular_rate, e.max_angular_rate);
+    viol = viol || (r != a[i]);
+    a[i] = r;
   }
   return viol;
 }
 
-// _check_termination (quadcopter_env.py:513-535)
+// _check_termination (quadcopter_env.py:513-535).  A finite sum of the 12
+// bounded components proves them all finite; a non-finite sum falls back to
+// the element test.
 __device__ __forceinline__ int termination(const qt_env_params& e, double t, const double* x) {
   if (t >= e.max_episode_time) return QT_TERM_TIME_LIMIT;
-  if (fabs(x[0]) > e.max_position || fabs(x[1]) > e.max_position || fabs(x[2]) > e.max_position)
-    return QT_TERM_POSITION_BOUNDS;
+  if (fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position) return QT_TERM_POSITION_BOUNDS;
+  double sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) sum += x[i];
+  if (isfinite(sum)) return QT_TERM_RUNNING;
   bool fin = true;
 #pragma unroll
   for (int i = 0; i < 12; ++i) fin = fin && isfinite(x[i]);
@@ -429,10 +465,16 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
   const double raw1 = uf[1] + -ffa[1];
   const double raw2 = uf[2] + ffa[0];
   const double raw3 = uf[3];
-  u[0] = clipd(raw0, c.min_thrust, c.max_thrust);
-  u[1] = clipd(raw1, -c.max_rate, c.max_rate);
-  u[2] = clipd(raw2, -c.max_rate, c.max_rate);
-  u[3] = clipd(raw3, -c.max_rate, c.max_rate);
+  u[0] = clip_num(raw0, c.min_thrust, c.max_thrust);
+  u[1] = clip_num(raw1, -c.max_rate, c.max_rate);
+  u[2] = clip_num(raw2, -c.max_rate, c.max_rate);
+  u[3] = clip_num(raw3, -c.max_rate, c.max_rate);
+  if (!isfinite((raw0 + raw1) + (raw2 + raw3))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
+    u[0] = raw0 != raw0 ? raw0 : u[0];
+    u[1] = raw1 != raw1 ? raw1 : u[1];
+    u[2] = raw2 != raw2 ? raw2 : u[2];
+    u[3] = raw3 != raw3 ? raw3 : u[3];
+  }
   if (diag) {  // get_control_components (riccati_lqr.py:946-954)
 #pragma unroll
     for (int i = 0; i < 6; ++i) diag[i] = s[i];

