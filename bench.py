@@ -179,8 +179,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: seeded reset draws (numpy default_rng per episode, as the reference), "
-                    "seeds = global episode index",
+            "data": "synthetic: seeded resets, seeds = global episode index; draws made on the GPU by the "
+                    "qt_seed_draws restatement of numpy default_rng (SeedSequence + PCG64 + ziggurat)",
             "config": {"workload": f"BASELINE configs[1]: {n} episodes/GPU x {nsteps - 2} steps, {args.motion} "
                                    f"target, Riccati-LQR shared K, RK4 dt=0.01",
                        "episodes_per_gpu": n, "episodes_total": n * world, "parallelism": f"episode-sharded x{world}"},

@@ -171,6 +171,14 @@ int qt_abi_version(void);
 int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset,
              qt_state st, void* stream);
 
+/* The per-episode draws of QuadcopterEnv.reset(seed) (quadcopter_env.py:122-137,
+   target_motion.py:318-366), reproducing numpy.random.default_rng(seed) on the
+   device (SeedSequence + PCG64 + numpy's ziggurat): pattern[4][n] in qt_batch
+   form and the start offset[3][n] of qt_reset.  seeds[n] >= 0; motion[n] or
+   NULL (then motion_default for all). */
+int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t motion_default,
+                  double* pattern, double* offset, void* stream);
+
 /* The fused closed loop: `nsteps` iterations of
    compute_action (riccati_lqr.py:779-967) -> env.step (quadcopter_env.py:152-232)
    per episode, register-resident, with the Evaluator's per-episode metric

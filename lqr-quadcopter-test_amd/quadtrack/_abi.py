@@ -79,7 +79,7 @@ class State(C.Structure):
                 ("target", C.c_void_p)]
 
 
-EXPORTS = ("qt_abi_version", "qt_reset", "qt_rollout", "qt_env_step", "qt_compute_action", "qt_target_state",
+EXPORTS = ("qt_abi_version", "qt_seed_draws", "qt_reset", "qt_rollout", "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary")
 
 _lib = None
@@ -100,6 +100,7 @@ def load():
     L = C.CDLL(LIB_PATH)
     P, vp, i32, i64, dbl = C.POINTER, C.c_void_p, C.c_int32, C.c_int64, C.c_double
     L.qt_abi_version.restype = C.c_int
+    L.qt_seed_draws.argtypes = [i64, vp, vp, i32, vp, vp, vp]
     L.qt_reset.argtypes = [P(EnvParams), P(Batch), vp, State, vp]
     L.qt_rollout.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, vp]
     L.qt_env_step.argtypes = [P(EnvParams), P(Batch), vp, State, vp, vp, vp, vp, vp, vp]

@@ -132,6 +132,22 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
             raise ValueError("batch tensors must be float64 on the batch device")
 
 
+def seed_draws(seeds: torch.Tensor, motion: torch.Tensor | None, motion_default: int):
+    """Device reset draws: seeds int64 [n] -> (pattern [4, n], offset [3, n])."""
+    lib = _abi.load()
+    n, dev = seeds.numel(), seeds.device
+    if seeds.dtype != torch.int64 or not seeds.is_contiguous():
+        raise ValueError("seeds must be a contiguous int64 tensor")
+    if n and int(seeds.min()) < 0:
+        raise ValueError("seeds must be non-negative (numpy SeedSequence)")
+    pat = torch.empty(4, n, dtype=F64, device=dev)
+    off = torch.empty(3, n, dtype=F64, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_seed_draws(n, ptr(seeds), ptr(motion), int(motion_default), ptr(pat), ptr(off),
+                                stream_of(dev)), "qt_seed_draws")
+    return pat, off
+
+
 def reset(env: EnvParams, batch: EpisodeBatch, st: RolloutState):
     lib = _abi.load()
     with torch.cuda.device(batch.device):

@@ -80,8 +80,8 @@ class BatchedQuadcopterEnv:
         seeds = np.asarray(seeds.cpu() if isinstance(seeds, torch.Tensor) else seeds, dtype=np.int64).reshape(-1)
         if seeds.size != self.num_envs:
             raise ValueError(f"{seeds.size} seeds for {self.num_envs} episodes")
-        kinds = self.motion.cpu().numpy() if self.motion is not None else self.config.motion_index()
-        pat, off = seeding.draws(kinds, seeds)
+        kinds = self.motion if self.motion is not None else self.config.motion_index()
+        pat, off = seeding.draws(kinds, seeds, self.device)
         return self.reset_from_draws(pat, off)
 
     # ----------------------------------------------------------------- step

@@ -95,7 +95,7 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
         if seeds.size != n:
             raise ValueError(f"{seeds.size} seeds for {n} episodes")
         kinds = motion_indices(motion, n) if motion is not None else cfg.motion_index()
-        draws = seeding.draws(kinds, seeds)
+        draws = seeding.draws(kinds, seeds, dev)
     pat, off = draws
     mo = None if motion is None else torch.as_tensor(motion_indices(motion, n), device=dev)
     pm = None if plant_mass is None else core.to_device(np.broadcast_to(np.asarray(plant_mass, float), (n,)), dev)
