@@ -179,6 +179,13 @@ int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offs
 int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t motion_default,
                   double* pattern, double* offset, void* stream);
 
+/* The first k draws of numpy.random.default_rng(seeds[e]).uniform(lo[j], hi[j])
+   for every episode e (per-episode parameters drawn from per-episode streams,
+   e.g. SURVEY §8d config 5's masses from default_rng(1e9 + i)).  lo, hi: [k]
+   DEVICE arrays; out[k][n]; k <= 64. */
+int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo, const double* hi,
+                    double* out, void* stream);
+
 /* The fused closed loop: `nsteps` iterations of
    compute_action (riccati_lqr.py:779-967) -> env.step (quadcopter_env.py:152-232)
    per episode, register-resident, with the Evaluator's per-episode metric
@@ -188,6 +195,15 @@ int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t
    rec[((s*16 + j) * n) + e] for j < 12 and the applied controller action at j = 12..15. */
 int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, void* stream);
+
+/* qt_rollout for a batch of mixed motion types, one motion-specialised launch
+   per group (no per-step motion dispatch).  batch->order must list the episodes
+   grouped by motion: slots [seg_end[i-1], seg_end[i]) (seg_end[-1] = 0) all
+   have motion seg_motion[i]; seg_end[nseg-1] == n.  seg_motion and seg_end are
+   HOST arrays.  Results are identical to qt_rollout's. */
+int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                       const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
+                       const int32_t* seg_motion, const int64_t* seg_end, void* stream);
 
 /* Open-loop QuadcopterEnv.step(action) for a batch (quadcopter_env.py:152-293):
    action[4][n] (NaN/Inf zeroed, thrust and rate clipping), RK4/Euler, state

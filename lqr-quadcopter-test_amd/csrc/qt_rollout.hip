@@ -77,6 +77,7 @@ struct BatchDev {
   const double* K;
   int32_t k_per_episode;
   const int32_t* order;
+  int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
 };
 
 __device__ __forceinline__ int64_t episode_of(const BatchDev& b, int64_t slot) {
@@ -166,8 +167,8 @@ template <int MOTION, int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec) {
-  const int64_t slot = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= b.n) return;
+  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.slot_end) return;
   const int64_t n = b.n, ep = episode_of(b, slot);
   const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
   const Pattern pt = pattern_of(b, e, motion, ep);
@@ -523,7 +524,8 @@ __global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const dou
 }
 
 BatchDev to_dev(const qt_batch* b) {
-  return BatchDev{b->n, b->motion, b->pattern, b->plant_mass, b->hover_thrust, b->K, b->k_per_episode, b->order};
+  return BatchDev{b->n, b->motion, b->pattern, b->plant_mass, b->hover_thrust, b->K, b->k_per_episode, b->order,
+                  0, b->n};
 }
 
 int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -605,6 +607,38 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   else
     launch_rollout<6>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   return check_launch();
+}
+
+int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                       const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
+                       const int32_t* seg_motion, const int64_t* seg_end, void* stream) {
+  if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
+  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (!valid_state(st, batch->k_cols == 9)) return QT_EINVAL;
+  if (nseg < 0 || (nseg > 0 && (!seg_motion || !seg_end))) return QT_EINVAL;
+  int64_t prev = 0;
+  for (int32_t i = 0; i < nseg; ++i) {
+    if (seg_end[i] < prev || seg_end[i] > batch->n || seg_motion[i] < 0 || seg_motion[i] > 4) return QT_EINVAL;
+    prev = seg_end[i];
+  }
+  if (prev != batch->n) return QT_EINVAL;
+  if (batch->n == 0 || nsteps == 0) return QT_OK;
+  BatchDev b = to_dev(batch);
+  hipStream_t s = (hipStream_t)stream;
+  const bool ff = ctrl->feedforward_enabled != 0;
+  const bool ks = batch->k_structured != 0;
+  for (int32_t i = 0; i < nseg; ++i) {
+    b.slot0 = i ? seg_end[i - 1] : 0;
+    b.slot_end = seg_end[i];
+    if (b.slot_end == b.slot0) continue;
+    const int grid = grid_of(b.slot_end - b.slot0);
+    if (batch->k_cols == 9)
+      launch_rollout<9>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    else
+      launch_rollout<6>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
+  }
+  return QT_OK;
 }
 
 int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action, qt_state st, double* err,

@@ -46,7 +46,26 @@ __global__ __launch_bounds__(256) void seed_draws_kernel(int64_t n, const int64_
   for (int i = 0; i < 3; ++i) offset[i * n + e] = -0.5 + 1.0 * qt::pcg_next_double(g);
 }
 
+// first k draws of default_rng(seed).uniform(lo[j], hi[j]) per episode
+__global__ __launch_bounds__(256) void seed_uniform_kernel(int64_t n, const int64_t* __restrict__ seeds, int32_t k,
+                                                           const double* __restrict__ lo,
+                                                           const double* __restrict__ hi, double* out) {
+#pragma clang fp contract(off)
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  qt::Pcg64 g = qt::pcg64_from_seed((uint64_t)seeds[e]);
+  for (int j = 0; j < k; ++j) out[(int64_t)j * n + e] = lo[j] + (hi[j] - lo[j]) * qt::pcg_next_double(g);
+}
+
 }  // namespace
+
+extern "C" int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo, const double* hi,
+                               double* out, void* stream) {
+  if (n < 0 || k < 0 || k > 64 || !seeds || !lo || !hi || !out) return QT_EINVAL;
+  if (n == 0 || k == 0) return QT_OK;
+  seed_uniform_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(n, seeds, k, lo, hi, out);
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
+}
 
 extern "C" int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t motion_default,
                              double* pattern, double* offset, void* stream) {

@@ -79,7 +79,8 @@ class State(C.Structure):
                 ("target", C.c_void_p)]
 
 
-EXPORTS = ("qt_abi_version", "qt_seed_draws", "qt_reset", "qt_rollout", "qt_env_step", "qt_compute_action", "qt_target_state",
+EXPORTS = ("qt_abi_version", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_grouped",
+           "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary")
 
 _lib = None
@@ -103,6 +104,9 @@ def load():
     L.qt_seed_draws.argtypes = [i64, vp, vp, i32, vp, vp, vp]
     L.qt_reset.argtypes = [P(EnvParams), P(Batch), vp, State, vp]
     L.qt_rollout.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, vp]
+    L.qt_rollout_grouped.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, i32,
+                                     P(C.c_int32), P(C.c_int64), vp]
+    L.qt_seed_uniform.argtypes = [i64, vp, i32, vp, vp, vp, vp]
     L.qt_env_step.argtypes = [P(EnvParams), P(Batch), vp, State, vp, vp, vp, vp, vp, vp]
     L.qt_compute_action.argtypes = [P(CtrlParams), P(Batch), vp, vp, vp, vp, vp, vp]
     L.qt_target_state.argtypes = [P(EnvParams), P(Batch), vp, vp, vp]

@@ -424,6 +424,8 @@ class BatchedRiccatiLQR:
         self.n_state = 9 if self.use_lqi else 6
         self.k_cols = self.n_state
         base_mass = float(config.get("mass", 1.0))
+        if isinstance(mass, torch.Tensor):
+            mass = mass.detach().to("cpu", torch.float64).numpy()
         per = [a is not None for a in (q_pos, q_vel, r_controls, q_int, mass, Q, R)]
         lens = [len(a) for a in (q_pos, q_vel, r_controls, q_int, mass, Q, R) if a is not None]
         if lens and len(set(lens)) != 1:
@@ -492,6 +494,23 @@ class BatchedRiccatiLQR:
 
     def riccati_solution(self) -> torch.Tensor:
         return self.P.T.reshape(-1, self.n_state, self.n_state)
+
+    def repeat_episodes(self, k: int) -> "BatchedRiccatiLQR":
+        """A view with every gain set used by k consecutive episodes (problem j
+        -> episodes j*k .. j*k+k-1): the tuner's candidates x evaluation
+        episodes (tuning.py:874-906) without re-solving any DARE."""
+        import copy
+
+        out = copy.copy(self)
+        if k == 1 and self.per_episode:
+            return out
+        rep = lambda t: None if t is None else t.repeat_interleave(k, dim=-1).contiguous()  # noqa: E731
+        out.K, out.P = rep(self.K), rep(self.P)
+        out.status, out.iters, out.mass, out.hover = rep(self.status), rep(self.iters), rep(self.mass), rep(self.hover)
+        out.num_problems = self.num_problems * k
+        out.per_episode = True
+        out.integral_state = None
+        return out
 
     def reset(self, n: int | None = None) -> None:
         n = n or self.num_problems

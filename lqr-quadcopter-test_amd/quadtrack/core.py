@@ -40,6 +40,7 @@ class EpisodeBatch:
     hover: torch.Tensor | None = None         # [n]
     order: torch.Tensor | None = None         # [n] int32
     k_structured: bool = False                # every off-axis K entry is exactly zero
+    groups: tuple | None = None               # (seg_motion, seg_end): `order` groups slots by motion
 
     def c_batch(self, with_k=True) -> Batch:
         b = Batch()
@@ -161,8 +162,44 @@ def rollout(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatc
     if rec is not None and (rec.numel() < nsteps * 16 * batch.n or rec.dtype != F64):
         raise ValueError("rec must hold nsteps * 16 * n float64")
     with torch.cuda.device(batch.device):
-        check(lib.qt_rollout(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()), st.c_state(),
-                             int(nsteps), ptr(rec), stream_of(batch.device)), "qt_rollout")
+        if batch.groups is not None:
+            seg_motion, seg_end = batch.groups
+            nseg = len(seg_motion)
+            sm = (C.c_int32 * nseg)(*[int(v) for v in seg_motion])
+            se = (C.c_int64 * nseg)(*[int(v) for v in seg_end])
+            check(lib.qt_rollout_grouped(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()),
+                                         st.c_state(), int(nsteps), ptr(rec), nseg, sm, se,
+                                         stream_of(batch.device)), "qt_rollout_grouped")
+        else:
+            check(lib.qt_rollout(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()), st.c_state(),
+                                 int(nsteps), ptr(rec), stream_of(batch.device)), "qt_rollout")
+
+
+def motion_groups(motion: np.ndarray):
+    """Host grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end)."""
+    motion = np.asarray(motion).reshape(-1)
+    order = np.argsort(motion, kind="stable").astype(np.int32)
+    kinds, counts = np.unique(motion, return_counts=True)
+    return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts)]
+
+
+def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:
+    """First k draws of default_rng(seed).uniform(lo[j], hi[j]) per seed -> [k, n]."""
+    lib = _abi.load()
+    n, dev = seeds.numel(), seeds.device
+    if seeds.dtype != torch.int64 or not seeds.is_contiguous():
+        raise ValueError("seeds must be a contiguous int64 tensor")
+    if n and int(seeds.min()) < 0:
+        raise ValueError("seeds must be non-negative (numpy SeedSequence)")
+    lo_t = to_device(np.atleast_1d(np.asarray(lo, float)), dev)
+    hi_t = to_device(np.atleast_1d(np.asarray(hi, float)), dev)
+    if lo_t.numel() != hi_t.numel() or lo_t.numel() > 64:
+        raise ValueError("lo and hi must have the same length k <= 64")
+    out = torch.empty(lo_t.numel(), n, dtype=F64, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.qt_seed_uniform(n, ptr(seeds), lo_t.numel(), ptr(lo_t), ptr(hi_t), ptr(out), stream_of(dev)),
+              "qt_seed_uniform")
+    return out
 
 
 def episode_metrics(crit: Criteria, st: RolloutState) -> torch.Tensor:

@@ -25,6 +25,14 @@ F64 = torch.float64
 
 def motion_indices(motion, n: int) -> np.ndarray:
     """Per-episode motion names / indices -> int8 array of enum qt_motion."""
+    if isinstance(motion, (np.ndarray, torch.Tensor)) and not (isinstance(motion, np.ndarray)
+                                                                and motion.dtype.kind in "UOS"):
+        a = np.asarray(motion.cpu() if isinstance(motion, torch.Tensor) else motion).reshape(-1)
+        if a.size != n:
+            raise ValueError(f"{a.size} motion types for {n} episodes")
+        if a.size and (a.min() < 0 or a.max() >= len(MOTIONS)):
+            raise ValueError(f"Invalid motion type index in {sorted(set(a.tolist()))[:8]}")
+        return a.astype(np.int8)
     out = np.empty(n, dtype=np.int8)
     vals = list(motion)
     if len(vals) != n:

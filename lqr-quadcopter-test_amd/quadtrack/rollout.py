@@ -83,7 +83,10 @@ class RolloutResult:
 
 
 def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, motion=None, plant_mass=None,
-                draws=None, device=None, order=None) -> core.EpisodeBatch:
+                draws=None, device=None, order=None, group_motion: bool = True) -> core.EpisodeBatch:
+    """Device inputs for `n` episodes.  Mixed motion types are grouped (one
+    motion-specialised launch per group, `qt_rollout_grouped`) unless an
+    explicit `order` is given or group_motion is False."""
     cfg = as_env_config(env_config)
     dev = _abi.require_gpu(device if device is not None else controller.device)
     if controller.per_episode and controller.num_problems != n:
@@ -97,12 +100,22 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
         kinds = motion_indices(motion, n) if motion is not None else cfg.motion_index()
         draws = seeding.draws(kinds, seeds, dev)
     pat, off = draws
-    mo = None if motion is None else torch.as_tensor(motion_indices(motion, n), device=dev)
-    pm = None if plant_mass is None else core.to_device(np.broadcast_to(np.asarray(plant_mass, float), (n,)), dev)
+    kinds = None if motion is None else motion_indices(motion, n)
+    mo = None if kinds is None else torch.as_tensor(kinds, device=dev)
+    groups = None
+    if kinds is not None and order is None and group_motion and len(np.unique(kinds)) > 1:
+        order, seg_motion, seg_end = core.motion_groups(kinds)
+        groups = (seg_motion, seg_end)
+    if plant_mass is None:
+        pm = None
+    elif isinstance(plant_mass, torch.Tensor) and plant_mass.numel() == n:
+        pm = core.to_device(plant_mass.reshape(-1), dev)
+    else:
+        pm = core.to_device(np.broadcast_to(np.asarray(plant_mass, float), (n,)), dev)
     od = None if order is None else torch.as_tensor(np.asarray(order, dtype=np.int32), device=dev)
     b = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pat, dev), offset=core.to_device(off, dev),
                           K=controller.K, k_cols=controller.k_cols, motion=mo, plant_mass=pm, hover=controller.hover,
-                          order=od, k_structured=controller.k_structured)
+                          order=od, k_structured=controller.k_structured, groups=groups)
     return b
 
 

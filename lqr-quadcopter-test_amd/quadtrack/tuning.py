@@ -1,0 +1,344 @@
+"""Batched controller-tuner evaluation (BASELINE config 4).
+
+The reference's `ControllerTuner` (controllers/tuning.py:581-1442) evaluates
+one candidate gain configuration at a time: `_evaluate_config` (846-928)
+builds one controller (one DARE), then runs `evaluation_episodes` fresh
+environments with seeds `seed + ep` (874-906), calling `controller.reset()`
+before each, and scores the candidate as
+`mean(on_target_ratio) - 0.1 * mean(mean_tracking_error)` (915-919).
+
+`BatchedTuner` evaluates every candidate of a sweep at once: all candidate
+DAREs in one batched SDA launch (`BatchedRiccatiLQR` with per-candidate
+q_pos / q_vel / r_controls / q_int), then candidates x episodes closed-loop
+episodes in one fused rollout, then per-candidate scores.  Candidate
+generation follows the reference's random stream exactly
+(`_generate_random_config` 683-735: `default_rng(seed)`, parameters in its
+fixed order, one `uniform(lo, hi)` per component) and its grid order
+(`_generate_grid_configs` 737-830).  Search strategies that need sequential
+feedback (CMA-ES), result files and resume are the tuner's control plane and
+stay out of scope.
+
+Supported controller_type: "riccati_lqr".  Feed-forward gain ranges need
+per-episode feed-forward gains, which the rollout kernel takes per batch, so
+they raise NotImplementedError.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field, fields
+from datetime import datetime, timezone
+from itertools import product
+
+import numpy as np
+import torch
+
+from .controllers.riccati_lqr import BatchedRiccatiLQR
+from .env.config import EnvConfig
+from .rollout import run_closed_loop
+from .utils.metrics import SuccessCriteria
+
+# parameter name -> (range attribute, components); the order of
+# _generate_random_config (tuning.py:689-733)
+_PARAM_ORDER = (
+    ("kp_pos", "kp_pos_range", 3),
+    ("ki_pos", "ki_pos_range", 3),
+    ("kd_pos", "kd_pos_range", 3),
+    ("ff_velocity_gain", "ff_velocity_gain_range", 3),
+    ("ff_acceleration_gain", "ff_acceleration_gain_range", 3),
+    ("q_pos", "q_pos_range", 3),
+    ("q_vel", "q_vel_range", 3),
+    ("r_thrust", "r_thrust_range", 0),
+    ("r_rate", "r_rate_range", 0),
+    ("r_controls", "r_controls_range", 4),
+    ("q_int", "q_int_range", 3),
+)
+
+
+@dataclass
+class GainSearchSpace:
+    """Search ranges (tuning.py:146-360): (min_values, max_values) per vector
+    parameter, (min, max) for the scalar r_thrust / r_rate; None = not tuned."""
+
+    kp_pos_range: tuple | None = None
+    ki_pos_range: tuple | None = None
+    kd_pos_range: tuple | None = None
+    ff_velocity_gain_range: tuple | None = None
+    ff_acceleration_gain_range: tuple | None = None
+    q_pos_range: tuple | None = None
+    q_vel_range: tuple | None = None
+    r_thrust_range: tuple | None = None
+    r_rate_range: tuple | None = None
+    r_controls_range: tuple | None = None
+    q_int_range: tuple | None = None
+    use_lqi: bool = False
+
+    def validate(self) -> None:
+        """Inverted or negative ranges and wrong lengths raise ValueError (tuning.py:194-298)."""
+        for name, attr, dim in _PARAM_ORDER:
+            rng = getattr(self, attr)
+            if rng is None:
+                continue
+            lo, hi = rng
+            if dim == 0:
+                lo, hi = [lo], [hi]
+            elif len(lo) != dim or len(hi) != dim:
+                raise ValueError(f"{attr} must have exactly {dim} values, got min={len(lo)}, max={len(hi)}")
+            for i, (a, b) in enumerate(zip(lo, hi)):
+                if a > b:
+                    raise ValueError(f"{attr}[{i}] has inverted range: min={a} > max={b}")
+                if a < 0:
+                    raise ValueError(f"{attr}[{i}] has negative minimum: {a}")
+
+    def get_active_parameters(self) -> list[str]:
+        out = [name for name, attr, _ in _PARAM_ORDER if getattr(self, attr) is not None]
+        if self.use_lqi and "q_int" not in out:
+            out.append("use_lqi")
+        return out
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "GainSearchSpace":
+        return cls(**{f.name: d.get(f.name, f.default) for f in fields(cls)})
+
+    def to_dict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+def default_search_space(controller_type: str = "riccati_lqr") -> GainSearchSpace:
+    """The Riccati-LQR ranges of scripts/controller_autotune.py:375-383 (config 4)."""
+    if controller_type != "riccati_lqr":
+        raise NotImplementedError(f"batched tuning supports riccati_lqr, not {controller_type!r}")
+    return GainSearchSpace(q_pos_range=([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0]),
+                           q_vel_range=([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0]),
+                           r_controls_range=([0.5] * 4, [2.0] * 4))
+
+
+@dataclass
+class TuningConfig:
+    """Tuner settings (tuning.py:363-478); same defaults."""
+
+    controller_type: str = "pid"
+    search_space: GainSearchSpace = field(default_factory=GainSearchSpace)
+    strategy: str = "random"
+    max_iterations: int = 50
+    grid_points_per_dim: int = 3
+    evaluation_episodes: int = 5
+    evaluation_horizon: int = 3000
+    seed: int = 42
+    target_motion_type: str = "stationary"
+    episode_length: float = 30.0
+    target_radius: float = 0.5
+    feedforward_enabled: bool = False
+
+    def __post_init__(self):
+        if self.controller_type not in ("pid", "lqr", "riccati_lqr"):
+            raise ValueError(f"Invalid controller_type: '{self.controller_type}'")
+        if self.strategy not in ("grid", "random", "cma_es"):
+            raise ValueError(f"Invalid strategy: '{self.strategy}'")
+        if self.max_iterations < 1:
+            raise ValueError(f"max_iterations must be >= 1, got {self.max_iterations}")
+        if self.evaluation_episodes < 1:
+            raise ValueError(f"evaluation_episodes must be >= 1, got {self.evaluation_episodes}")
+
+
+@dataclass
+class TuningResult:
+    """tuning.py:480-532 (no file I/O here)."""
+
+    best_config: dict
+    best_score: float
+    best_metrics: dict
+    all_results: list
+    iterations_completed: int
+    interrupted: bool
+    timestamp: str
+    config: dict
+
+    def to_dict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+def random_configs(space: GainSearchSpace, n: int, rng: np.random.Generator) -> list[dict]:
+    """n consecutive `_generate_random_config` results from `rng` (tuning.py:683-735).
+
+    One vectorised draw of [n, D] uniforms: numpy fills it in C order from
+    the same stream, lo + (hi - lo) * next_double per element, which is what
+    the reference's D scalar `rng.uniform(lo, hi)` calls per candidate do."""
+    cols, spec = [], []
+    for name, attr, dim in _PARAM_ORDER:
+        rng_def = getattr(space, attr)
+        if rng_def is None:
+            continue
+        lo, hi = rng_def
+        lo, hi = ([lo], [hi]) if dim == 0 else (list(lo), list(hi))
+        spec.append((name, len(cols), dim))
+        cols.extend(zip(lo, hi))
+    if not cols:
+        u = np.empty((n, 0))
+    else:
+        lo = np.array([c[0] for c in cols], float)
+        hi = np.array([c[1] for c in cols], float)
+        u = rng.uniform(lo, hi, size=(n, len(cols)))
+    out = []
+    for i in range(n):
+        cfg = {}
+        for name, j, dim in spec:
+            cfg[name] = float(u[i, j]) if dim == 0 else [float(v) for v in u[i, j:j + dim]]
+            if name in ("ff_velocity_gain", "ff_acceleration_gain"):
+                cfg["feedforward_enabled"] = True
+            if name == "q_int":
+                cfg["use_lqi"] = True
+        if space.q_int_range is None and space.use_lqi:
+            cfg["use_lqi"] = True
+            cfg["q_int"] = [0.0, 0.0, 0.0]
+        out.append(cfg)
+    return out
+
+
+def grid_configs(space: GainSearchSpace, points: int) -> list[dict]:
+    """The reference's grid (tuning.py:737-830): per-axis linspace (a single
+    point where lo == hi), Cartesian products in parameter order."""
+
+    def axis(lo, hi):
+        return [lo] if np.isclose(lo, hi) else list(np.linspace(lo, hi, points))
+
+    grids = {}
+    for name, attr, dim in _PARAM_ORDER:
+        rng_def = getattr(space, attr)
+        if rng_def is None:
+            if name == "q_int" and space.use_lqi:
+                grids[name] = [[0.0, 0.0, 0.0]]
+            continue
+        lo, hi = rng_def
+        if dim == 0:
+            grids[name] = axis(lo, hi)
+        else:
+            grids[name] = [list(c) for c in product(*[axis(a, b) for a, b in zip(lo, hi)])]
+    if not grids:
+        return []
+    names = list(grids)
+    out = []
+    for combo in product(*[grids[k] for k in names]):
+        cfg = dict(zip(names, combo))
+        if "ff_velocity_gain" in cfg or "ff_acceleration_gain" in cfg:
+            cfg["feedforward_enabled"] = True
+        if "q_int" in cfg or space.use_lqi:
+            cfg["use_lqi"] = True
+        out.append(cfg)
+    return out
+
+
+class BatchedTuner:
+    """`ControllerTuner` with every candidate evaluated in one batch.
+
+    evaluate_configs(configs) -> [(score, metrics)] in candidate order, the
+    values `_evaluate_config` returns for each (tuning.py:846-928)."""
+
+    def __init__(self, config: TuningConfig, device=None, base_controller_config: dict | None = None):
+        if config.controller_type != "riccati_lqr":
+            raise NotImplementedError(f"batched tuning supports riccati_lqr, not {config.controller_type!r}")
+        config.search_space.validate()
+        self.config = config
+        self.device = device
+        self.base = dict(base_controller_config or {})
+        self.rng = np.random.default_rng(config.seed)
+        self.results: list[dict] = []
+        self.best_config: dict = {}
+        self.best_score = float("-inf")
+        self.best_metrics: dict = {}
+
+    # ---- candidate generation (reference stream order)
+    def generate_random_configs(self, n: int) -> list[dict]:
+        return random_configs(self.config.search_space, n, self.rng)
+
+    def generate_grid_configs(self) -> list[dict]:
+        return grid_configs(self.config.search_space, self.config.grid_points_per_dim)
+
+    # ---- evaluation
+    def env_config(self) -> EnvConfig:
+        """tuning.py:859-863."""
+        env = EnvConfig()
+        env.simulation.max_episode_time = self.config.episode_length
+        env.target.motion_type = self.config.target_motion_type
+        env.success_criteria.target_radius = self.config.target_radius
+        return env
+
+    def criteria(self) -> SuccessCriteria:
+        """tuning.py:865-869."""
+        return SuccessCriteria(min_on_target_ratio=0.8, min_episode_duration=self.config.episode_length,
+                               target_radius=self.config.target_radius)
+
+    def controller(self, configs: list[dict]) -> BatchedRiccatiLQR:
+        """One batched DARE over the candidates (one problem per candidate)."""
+        keys = set().union(*[c.keys() for c in configs]) if configs else set()
+        unsupported = keys & {"ff_velocity_gain", "ff_acceleration_gain", "kp_pos", "ki_pos", "kd_pos",
+                              "r_thrust", "r_rate"}
+        if unsupported:
+            raise NotImplementedError(f"per-candidate {sorted(unsupported)} are not batched")
+        lqi = {bool(c.get("use_lqi", False)) for c in configs}
+        if len(lqi) > 1:
+            raise ValueError("candidates mix LQR and LQI")
+        shared = dict(self.base)
+        shared["use_lqi"] = lqi.pop() if lqi else False
+
+        def col(key, default):
+            d = np.asarray(shared.get(key, default), float)
+            return np.stack([np.asarray(c.get(key, d), float) for c in configs])
+
+        kw = dict(q_pos=col("q_pos", [1e-4, 1e-4, 16.0]), q_vel=col("q_vel", [0.0036, 0.0036, 4.0]),
+                  r_controls=col("r_controls", [1.0] * 4))
+        if shared["use_lqi"]:
+            kw["q_int"] = col("q_int", [0.0, 0.0, 0.0])
+        return BatchedRiccatiLQR(shared, device=self.device, **kw)
+
+    def evaluate_configs(self, configs: list[dict], chunk: int | None = None):
+        """Scores and metrics of every candidate (tuning.py:846-928)."""
+        if not configs:
+            return []
+        E = self.config.evaluation_episodes
+        ctl = self.controller(configs).repeat_episodes(E)
+        seeds = np.tile(self.config.seed + np.arange(E, dtype=np.int64), len(configs))
+        res = run_closed_loop(ctl, self.env_config(), n=len(seeds), seeds=seeds, criteria=self.criteria(),
+                              max_steps=self.config.evaluation_horizon, chunk=chunk)
+        m = res.metrics.cpu().numpy()
+        from ._abi import MET
+
+        C = len(configs)
+        ratio = m[MET["on_target_ratio"]].reshape(C, E)
+        err = m[MET["mean_tracking_error"]].reshape(C, E)
+        succ = m[MET["success"]].reshape(C, E)
+        out = []
+        for c in range(C):
+            mean_on = np.mean(list(ratio[c]))
+            mean_err = np.mean(list(err[c]))
+            rate = np.mean(list(succ[c]))
+            score = mean_on - 0.1 * mean_err
+            out.append((float(score), {"mean_on_target_ratio": float(mean_on), "mean_tracking_error": float(mean_err),
+                                       "success_rate": float(rate), "episodes_evaluated": E}))
+        return out
+
+    def _record(self, cfg, score, metrics):
+        """tuning.py:1075-1088 (strictly-greater best update)."""
+        self.results.append({"config": cfg, "score": score, "metrics": metrics})
+        if score > self.best_score:
+            self.best_score, self.best_config, self.best_metrics = score, cfg, metrics
+
+    def tune(self) -> TuningResult:
+        """Random or grid search with all candidates evaluated in one batch."""
+        if self.config.strategy == "cma_es":
+            raise NotImplementedError("CMA-ES is sequential; out of scope for the batched tuner")
+        if self.config.strategy == "grid":
+            configs = self.generate_grid_configs()[:self.config.max_iterations]
+        else:
+            configs = self.generate_random_configs(self.config.max_iterations - len(self.results))
+        for cfg, (score, metrics) in zip(configs, self.evaluate_configs(configs)):
+            self._record(cfg, score, metrics)
+        cfg_dict = {f.name: getattr(self.config, f.name) for f in fields(self.config)}
+        cfg_dict["search_space"] = self.config.search_space.to_dict()
+        return TuningResult(best_config=self.best_config, best_score=self.best_score,
+                            best_metrics=self.best_metrics, all_results=self.results,
+                            iterations_completed=len(self.results), interrupted=False,
+                            timestamp=datetime.now(timezone.utc).isoformat(), config=cfg_dict)
+
+
+__all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "random_configs", "grid_configs",
+           "default_search_space"]

@@ -157,21 +157,27 @@ def test_chunked_equals_single_launch(qt):
 
 
 def test_mixed_motion_order_permutation(qt):
-    """A per-episode `order` (group episodes by motion) does not change results."""
-    from quadtrack import core
+    """Mixed motion types: the per-step runtime-motion kernel, the same kernel
+    under a permuting `order`, and the grouped motion-specialised launches
+    (qt_rollout_grouped, the default) give identical results."""
     from quadtrack.controllers import BatchedRiccatiLQR
     from quadtrack.rollout import build_batch, run_closed_loop
 
     n = 2000
     motion = [i % 5 for i in range(n)]
     ctl = BatchedRiccatiLQR({"dt": 0.01})
-    a = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
-    order = np.argsort(np.array(motion), kind="stable")
+    plain = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, group_motion=False)
+    assert plain.groups is None
+    a = run_closed_loop(ctl, {}, n=n, batch=plain, max_steps=500)
+    order = np.random.default_rng(3).permutation(n)
     b = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, order=order)
+    assert b.groups is None
     r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
-    assert torch.equal(a.metrics, r.metrics)
-    assert torch.equal(a.state.x, r.state.x)
-    assert core is not None
+    g = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
+    assert g.batch.groups is not None and len(g.batch.groups[0]) == 5
+    for other in (r, g):
+        assert torch.equal(a.metrics, other.metrics)
+        assert torch.equal(a.state.x, other.state.x)
 
 
 # -------------------------------------------------------------------- DARE

@@ -1,0 +1,155 @@
+"""BASELINE.json configs 3-5 on the GPU (quadtrack.workloads) against the
+oracle on seeded samples, plus shard independence.
+
+Each sample is a shard [lo, lo + n) taken from the middle of the config's
+global episode range, so the per-episode inputs exercise the global-index
+functions (tuner stream advanced to candidate lo, mass seeds 1e9 + i, motion
+i mod 5).  The oracle side derives every per-episode input independently:
+Q/R from the reference tuner's sequential draws, K from its own DARE, masses
+from numpy default_rng, reset draws from numpy.  Tolerance as in
+test_gpu_parity: 1e-5 absolute (north star), 1e-8 relative.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def qt():
+    import quadtrack
+
+    quadtrack._abi.require_gpu()
+    return quadtrack
+
+
+def _tuner_stream(lo, hi):
+    """The reference's _generate_random_config (tuning.py:683-735) called hi
+    times on default_rng(42), sequential scalar draws; candidates lo..hi-1."""
+    r = np.random.default_rng(42)
+    out = []
+    for _ in range(hi):
+        qp = [float(r.uniform(a, b)) for a, b in zip([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0])]
+        qv = [float(r.uniform(a, b)) for a, b in zip([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0])]
+        rc = [float(r.uniform(0.5, 2.0)) for _ in range(4)]
+        out.append({"q_pos": qp, "q_vel": qv, "r_controls": rc})
+    return out[lo:]
+
+
+def _oracle_shard(config, lo, hi):
+    """(met[n,14], xf[n,12]) of episodes lo..hi-1 of `config` by the oracle."""
+    idx = np.arange(lo, hi)
+    n = len(idx)
+    motion = {3: 3, 4: 2}.get(config)
+    motions = idx % 5 if config == 5 else np.full(n, motion)
+    env = O.env_params({"target": {"motion_type": O.MOTIONS[motions[0]]}})
+    pat = np.zeros((n, 4))
+    off = np.zeros((n, 3))
+    for m in np.unique(motions):
+        sel = motions == m
+        pat[sel], off[sel] = O.draws(int(m), idx[sel])
+    x0 = np.array([O.initial_state(env, int(motions[i]), pat[i], off[i]) for i in range(n)])
+    mass = hover = None
+    if config == 3:
+        c, K, kc, _, _ = O.controller({"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2],
+                                       "integral_limit": 10.0, "integral_zero_threshold": 0.01})
+        per = False
+    elif config == 4:
+        Ks = []
+        for cand in _tuner_stream(lo, hi):
+            c, K, kc, fb, _ = O.controller(dict(cand, dt=0.01))
+            assert not fb
+            Ks.append(K)
+        K, per = np.array(Ks), True
+    else:
+        mass = np.array([np.random.default_rng(10**9 + int(i)).uniform(0.8, 1.2) for i in idx])
+        Ks = []
+        for m in mass:
+            c, K, kc, fb, _ = O.controller({"dt": 0.01, "mass": float(m)})
+            Ks.append(K)
+        K, per = np.array(Ks), True
+        hover = mass * 9.81
+    mo = motions.astype(np.int8) if config == 5 else None
+    met, xf, integ, _ = O.rollout(env, c, O.criteria(), mo, pat, mass, hover, K, kc, per, x0)
+    return met, xf, mass
+
+
+@pytest.mark.parametrize("config,lo,n", [(3, 40000, 384), (4, 200001, 384), (5, 777777, 640)])
+def test_workload_sample_vs_oracle(qt, config, lo, n):
+    from quadtrack import workloads
+    from quadtrack.rollout import run_closed_loop
+
+    sh = workloads.build(config, lo, lo + n)
+    res = run_closed_loop(sh.controller, **sh.run_kwargs())
+    met = res.metrics.cpu().numpy()
+    om, oxf, mass = _oracle_shard(config, lo, lo + n)
+    if mass is not None:
+        np.testing.assert_array_equal(sh.plant_mass.cpu().numpy(), mass)  # device draws == numpy, bit for bit
+    np.testing.assert_allclose(met.T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(res.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=TOL)
+
+
+@pytest.mark.parametrize("config", [4, 5])
+def test_workload_full_size_and_shard_independence(qt, config):
+    """The whole config on one GPU; then a 4-way sharding of it reproduces
+    every per-episode metric bit for bit (results independent of W)."""
+    from quadtrack import workloads
+    from quadtrack._abi import MET
+    from quadtrack.rollout import run_closed_loop
+
+    total = workloads.EPISODES[config]
+    full = workloads.build(config)
+    res = run_closed_loop(full.controller, **full.run_kwargs())
+    met = res.metrics
+    assert bool(torch.isfinite(met).all())
+    assert int((met[MET["termination_code"]] == 0).sum()) == 0  # every episode terminated
+    if config == 5:
+        assert full.controller.status.eq(0).all()
+    for r in range(4):
+        lo, hi = workloads.shard_bounds(total, r, 4)
+        if r not in (0, 3):
+            continue  # two shards are enough to pin the property; keeps the test short
+        sh = workloads.build(config, lo, hi)
+        part = run_closed_loop(sh.controller, **sh.run_kwargs())
+        assert torch.equal(part.metrics, met[:, lo:hi])
+    del res, full
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("horizon", [450, 3000])
+def test_batched_tuner_vs_sequential_oracle(qt, horizon):
+    """BatchedTuner.tune() (all candidates x episodes in one rollout) against
+    the reference tuner's loop restated on the oracle: per candidate one
+    controller, evaluation_episodes fresh episodes with seeds seed + ep
+    (tuning.py:846-928), score = mean ratio - 0.1 mean error."""
+    from quadtrack import tuning
+
+    cfg = tuning.TuningConfig(controller_type="riccati_lqr", search_space=tuning.default_search_space(),
+                              max_iterations=24, evaluation_episodes=3, target_motion_type="circular",
+                              episode_length=5.0, evaluation_horizon=horizon, seed=42)
+    res = tuning.BatchedTuner(cfg).tune()
+    assert res.iterations_completed == 24
+    cands = _tuner_stream(0, 24)
+    env = O.env_params({"simulation": {"max_episode_time": 5.0}, "target": {"motion_type": "circular"}})
+    crit = O.criteria(0.8, 5.0, 0.5)
+    seeds = 42 + np.arange(3)
+    pat, off = O.draws("circular", seeds)
+    x0 = np.array([O.initial_state(env, 2, pat[i], off[i]) for i in range(3)])
+    best = -np.inf
+    for k, cand in enumerate(cands):
+        assert res.all_results[k]["config"] == cand
+        c, K, kc, _, _ = O.controller(dict(cand, dt=0.01))
+        met, _, _, _ = O.rollout(env, c, crit, None, pat, None, None, K, kc, False, x0, max_steps=horizon)
+        ratio = met[:, O.MET_FIELDS.index("on_target_ratio")]
+        err = met[:, O.MET_FIELDS.index("mean_tracking_error")]
+        score = np.mean(list(ratio)) - 0.1 * np.mean(list(err))
+        got = res.all_results[k]
+        assert got["score"] == pytest.approx(score, rel=1e-9, abs=1e-9)
+        assert got["metrics"]["mean_on_target_ratio"] == pytest.approx(np.mean(list(ratio)), abs=1e-12)
+        best = max(best, score)
+    assert res.best_score == pytest.approx(best, rel=1e-9, abs=1e-9)
