@@ -184,9 +184,11 @@ __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 // sin(a + d) = sin a cos d + cos a sin d,  cos(a + d) = cos a cos d - sin a sin d,
 // with sin d / cos d from small_sincos.  The stage offsets are h * (body rate)
 // <= dt * ~12 rad/s; an offset beyond the polynomial's range takes fast_sincos.
+// SMALL: the caller has proven |delta| <= kSmallAngle (small_angle_bound).
+template <bool SMALL = false>
 __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t) {
-  const double dm = fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
-  if (dm <= kSmallAngle) {
+  const double dm = SMALL ? 0.0 : fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
+  if (SMALL || dm <= kSmallAngle) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       double sd, cd;
@@ -222,13 +224,15 @@ __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant&
 
 // _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held
 // constant across the four stages.
+// FAST: RK4 known (integrator == 0) and every stage offset proven small.
+template <bool FAST = false>
 __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
   const double dt = e.dt;
   double k[12];
   Trig t0, ts;
   trig_of(x + 6, t0);
   derivatives(e, pl, x, u, t0, k);
-  if (e.integrator == 1) {
+  if (!FAST && e.integrator == 1) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
     return;
@@ -245,7 +249,7 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
-  trig_shift(x + 6, t0, del, ts);
+  trig_shift<FAST>(x + 6, t0, del, ts);
   derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -254,7 +258,7 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
-  trig_shift(x + 6, t0, del, ts);
+  trig_shift<FAST>(x + 6, t0, del, ts);
   derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -263,7 +267,7 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i) del[i] = dt * k[6 + i];
-  trig_shift(x + 6, t0, del, ts);
+  trig_shift<FAST>(x + 6, t0, del, ts);
   derivatives(e, pl, tmp, u, ts, k);
   const double h6 = dt / 6.0;
 #pragma unroll
@@ -357,6 +361,79 @@ __device__ __forceinline__ int termination(const qt_env_params& e, double t, con
   return fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY;
 }
 
+// ------------------------------------------------- fast-path preconditions
+//
+// The fused rollout has a branch-light variant of the step (the "fast path")
+// that takes the same decisions as the exact one and computes the same
+// expressions (up to the compiler's FMA contraction) whenever these hold:
+//  * RK4 integration;
+//  * the controller's clamps lie inside the env's action clamps, so
+//    _parse_and_validate_action never clips or flags a finite command;
+//  * every RK4 stage attitude offset is within small_sincos' range: the body
+//    rates start a step within +-max_angular_velocity (constrained every step)
+//    and the commanded rates within +-max_angular_rate, which bounds the stage
+//    rates through the first-order rate dynamics (quadcopter_env.py:412-421);
+//  * per lane: finite gains, hover thrust and state (checked at kernel entry).
+__host__ __device__ inline double small_angle_bound(const qt_env_params& e) {
+  const double h2 = 0.5 * e.dt, w = e.max_angular_velocity, r = e.max_angular_rate, cd = fabs(e.drag_angular);
+  const double k1 = (r + w) * 10.0 + cd * w;     // |d omega / dt| at stage 1
+  const double w2 = w + h2 * k1;                  // |omega| at stages 2, 3
+  const double k2 = (r + w2) * 10.0 + cd * w2;
+  const double w3 = w + h2 * k2;                  // |omega| at stage 3 (offset of stage 4)
+  return fmax(h2 * w2, e.dt * w3) * (1.0 + 1e-12);
+}
+
+__host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ctrl_params& c) {
+  return e.integrator == 0 && c.min_thrust >= e.min_thrust && c.max_thrust <= e.max_thrust &&
+         c.min_thrust <= c.max_thrust && c.max_rate <= e.max_angular_rate && c.max_rate >= 0.0 &&
+         e.max_angular_velocity >= 0.0 && small_angle_bound(e) <= kSmallAngle;
+}
+
+// Fast-path state constraints: the common case of _apply_state_constraints
+// without branches.  constrain_fast_ok is false when the exact path is
+// needed: speed within 1e-14 of the clamp or above it, or an attitude angle
+// with (a + pi) outside (-2 pi, 4 pi), where numpy's floor-mod takes more
+// than one correction (or the state is not finite).
+__device__ __forceinline__ bool constrain_fast_ok(const qt_env_params& e, const double* x) {
+  const double sv = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
+  const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
+  bool ok = sv < vm2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double b = x[6 + i] + kPi;
+    ok = ok & (b > -kTwoPi) & (b < 2.0 * kTwoPi);
+  }
+  return ok;
+}
+
+__device__ __forceinline__ void constrain_fast_apply(const qt_env_params& e, double* x) {
+#pragma unroll
+  for (int i = 9; i < 12; ++i) x[i] = clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    // (b % 2 pi) for b in (-2 pi, 4 pi): one correction, the same rounding as
+    // numpy's (b < 0: b + 2 pi; b >= 2 pi: b - 2 pi, exact by Sterbenz)
+    const double b = x[6 + i] + kPi;
+    const double adj = b < 0.0 ? kTwoPi : (b >= kTwoPi ? -kTwoPi : 0.0);
+    x[6 + i] = (b + adj) - kPi;
+  }
+  x[6] = clip_num(x[6], -kMaxTilt, kMaxTilt);
+  x[7] = clip_num(x[7], -kMaxTilt, kMaxTilt);
+}
+
+// _check_termination without branches for a state whose components are
+// bounded when finite (inside the fused rollout): a non-finite sum of the 12
+// components then means a non-finite component.
+__device__ __forceinline__ int termination_fast(const qt_env_params& e, double t, const double* x) {
+  const bool tl = t >= e.max_episode_time;
+  const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
+  double sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) sum += x[i];
+  const int fin = isfinite(sum) ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY;
+  return tl ? QT_TERM_TIME_LIMIT : (pb ? QT_TERM_POSITION_BOUNDS : fin);
+}
+
 // ------------------------------------------------------------ controller
 
 // Gains as seen by one lane, loaded once per launch.  Dense: the full 4 x KC
@@ -384,7 +461,9 @@ __host__ __device__ constexpr int structured_index(int j) {
 // RiccatiLQRController.compute_action (riccati_lqr.py:779-967) given the
 // observation the env returned (quad p, v; target p, v, a).  LQI integral
 // update 869-900, output clamps 907-921.  Returns true when saturated.
-template <int KC, bool FF, bool KS>
+// FAST: gains, hover thrust and observation are known finite, so the raw
+// command is finite and np.clip's NaN pass-through cannot arise.
+template <int KC, bool FF, bool KS, bool FAST = false>
 __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC, KS>& G, double hover,
                                                const double* qp, const double* qv, const Target& tg,
                                                double* integ, double* u, double* diag = nullptr) {
@@ -469,7 +548,7 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
   u[1] = clip_num(raw1, -c.max_rate, c.max_rate);
   u[2] = clip_num(raw2, -c.max_rate, c.max_rate);
   u[3] = clip_num(raw3, -c.max_rate, c.max_rate);
-  if (!isfinite((raw0 + raw1) + (raw2 + raw3))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
+  if (!FAST && !isfinite((raw0 + raw1) + (raw2 + raw3))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
     u[0] = raw0 != raw0 ? raw0 : u[0];
     u[1] = raw1 != raw1 ? raw1 : u[1];
     u[2] = raw2 != raw2 ? raw2 : u[2];

@@ -117,17 +117,16 @@ __device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<
 __device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int window) {
   // Branch-free form of the three transitions (metrics.py:238-254).  `start`
   // (previous step on target, this one off) and `in_phase` (previous step
-  // off target inside a phase) exclude each other.
+  // off target inside a phase) exclude each other.  os_cur is only read
+  // inside a phase; outside one it holds -inf after an on-target step (so a
+  // phase start takes `over` through the same max) and is otherwise unused.
   const bool in_phase = a.os_streak >= 0;
   const bool start = (a.prev_on > 0) && !on;
-  const bool cont = in_phase && !on;
-  const bool close = in_phase && on;
-  const bool counted = close && a.os_streak >= window;
+  const bool counted = on && in_phase && a.os_streak >= window;
   a.os_count += counted;
-  a.os_max = (counted && a.os_cur > a.os_max) ? a.os_cur : a.os_max;
-  const double cur_cont = over > a.os_cur ? over : a.os_cur;
-  a.os_cur = start ? over : (cont ? cur_cont : (close ? 0.0 : a.os_cur));
-  a.os_streak = start ? 1 : (cont ? a.os_streak + 1 : (close ? -1 : a.os_streak));
+  a.os_max = counted ? fmax(a.os_max, a.os_cur) : a.os_max;
+  a.os_cur = on ? -INFINITY : fmax(over, a.os_cur);
+  a.os_streak = on ? -1 : (start ? 1 : (in_phase ? a.os_streak + 1 : -1));
 }
 
 // ------------------------------------------------------------------ reset
@@ -162,6 +161,93 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev
 
 // ---------------------------------------------------------------- rollout
 
+// The closed-loop steps of one lane.  FAST: the branch-light step of
+// qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
+// takes the exact step's decisions; rare lanes/steps (speed at the
+// clamp, attitude far outside [-pi, pi), tracking error at the radius within
+// 1e-14) fall back to the exact constraint / comparison code inside the step.
+template <bool FAST, int MOTION, int KC, bool FF, bool KS>
+__device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
+                                          int motion, const Pattern& pt, const Plant& pl, double hover,
+                                          const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
+                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep) {
+  const double R = cr.target_radius;
+  const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
+  const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
+  for (int s = 0; s < nsteps; ++s) {
+    if (a.term != QT_TERM_RUNNING) break;
+    // ---- compute_action on the current observation (riccati_lqr.py:779-967)
+    double u[4];
+    if (QT_ABLATE & QT_ABL_CONTROLLER) {
+      u[0] = hover, u[1] = u[2] = u[3] = 0.0;
+    } else {
+      compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u);
+    }
+    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
+    if (!(QT_ABLATE & QT_ABL_METRICS)) {
+      const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+      const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+      a.sum_e += err;
+      a.sum_e2 += err * err;
+      if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
+      const bool on = err <= R;
+      a.on_pre += on;
+      a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
+      a.prev_on = on;
+    }
+    // ---- env.step (quadcopter_env.py:152-232)
+    if (FAST) {
+      // the command is finite and inside the env clamps: parsing is the identity
+      integrate<true>(e, pl, x, u);
+      t += e.dt;
+      if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
+      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+      const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
+      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok(e, x));
+      if (ok) {
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply(e, x);
+        a.on_post += se < er2lo;
+      } else {  // rare: exact constraints and comparison
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
+        a.on_post += norm_le(se, e.target_radius);
+      }
+      if (QT_ABLATE & QT_ABL_TERMINATION)
+        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
+      else
+        a.term = termination_fast(e, t, x);
+      a.steps += 1;
+    } else {
+      double ua[4];
+      a.viol += parse_action(e, u, ua);
+      integrate(e, pl, x, ua);
+      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
+      t += e.dt;
+      if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
+      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+      a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
+      if (QT_ABLATE & QT_ABL_TERMINATION)
+        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
+      else
+        a.term = termination(e, t, x);
+      a.steps += 1;
+      if (rec) {
+        double* r = rec + (int64_t)s * 16 * n + ep;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r[i * n] = x[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[(12 + i) * n] = u[i];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool all_finite(const double* v, int k) {
+  double s = 0.0;
+  for (int i = 0; i < k; ++i) s += v[i] * 0.0;  // NaN iff some v[i] is NaN or infinite
+  return s == 0.0;
+}
+
 // MOTION >= 0 specialises the target pattern; -1 reads it per episode.
 template <int MOTION, int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
@@ -193,52 +279,20 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   }
   double t = st.t[ep];
   Acc a = load_acc(st.acc, n, ep);
-  const double R = cr.target_radius;
 
-  for (int s = 0; s < nsteps; ++s) {
-    if (a.term != QT_TERM_RUNNING) break;
-    // ---- compute_action on the current observation (riccati_lqr.py:779-967)
-    double u[4];
-    if (QT_ABLATE & QT_ABL_CONTROLLER) {
-      u[0] = hover, u[1] = u[2] = u[3] = 0.0;
-    } else {
-      compute_action<KC, FF, KS>(c, G, hover, x, x + 3, tg, integ, u);
-    }
-    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
-    if (!(QT_ABLATE & QT_ABL_METRICS)) {
-      const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-      const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
-      a.sum_e += err;
-      a.sum_e2 += err * err;
-      if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
-      const bool on = err <= R;
-      a.on_pre += on;
-      a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
-      overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
-      a.prev_on = on;
-    }
-    // ---- env.step (quadcopter_env.py:152-232)
-    double ua[4];
-    a.viol += parse_action(e, u, ua);
-    integrate(e, pl, x, ua);
-    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
-    t += e.dt;
-    if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
-    const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
-    a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
-    if (QT_ABLATE & QT_ABL_TERMINATION)
-      a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
-    else
-      a.term = termination(e, t, x);
-    a.steps += 1;
-    if (rec) {
-      double* r = rec + (int64_t)s * 16 * n + ep;
-#pragma unroll
-      for (int i = 0; i < 12; ++i) r[i * n] = x[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) r[(12 + i) * n] = u[i];
-    }
-  }
+  // fast path for the whole wavefront when every lane qualifies (uniform branch)
+  bool lane_ok = a.term != QT_TERM_RUNNING ||
+                 (all_finite(G.k, Gains<KC, KS>::kCount) && all_finite(x, 12) && all_finite(integ, 3) &&
+                  all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && isfinite(hover) &&
+                  isfinite(pl.inv_mass) && fabs(t) < 1e300);
+  for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
+  const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c) &&
+                    __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
+  if (fast)
+    run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n, ep);
+  else
+    run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n,
+                                         ep);
 
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];

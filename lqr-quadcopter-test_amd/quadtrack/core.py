@@ -94,7 +94,7 @@ def gains_structured(K: torch.Tensor, k_cols: int) -> bool:
 def to_device(a, device, dtype=F64) -> torch.Tensor:
     if isinstance(a, torch.Tensor):
         return a.to(device=device, dtype=dtype).contiguous()
-    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device).contiguous()
+    return torch.as_tensor(np.require(a, requirements=["C", "W"]), dtype=dtype, device=device).contiguous()
 
 
 def _check_cols(name, t, rows, n):

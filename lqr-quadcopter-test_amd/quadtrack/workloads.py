@@ -77,6 +77,18 @@ def tuner_candidates(lo: int, hi: int, seed: int = TUNER_SEED) -> list[dict]:
     return random_configs(default_search_space("riccati_lqr"), hi - lo, rng)
 
 
+def tuner_candidate_arrays(lo: int, hi: int, seed: int = TUNER_SEED) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """tuner_candidates as arrays (q_pos [n,3], q_vel [n,3], r_controls [n,4]),
+    same stream, no per-candidate dicts."""
+    space = default_search_space("riccati_lqr")
+    lo_v = np.array(list(space.q_pos_range[0]) + list(space.q_vel_range[0]) + list(space.r_controls_range[0]))
+    hi_v = np.array(list(space.q_pos_range[1]) + list(space.q_vel_range[1]) + list(space.r_controls_range[1]))
+    rng = np.random.default_rng(seed)
+    rng.bit_generator.advance(TUNER_DRAWS_PER_CANDIDATE * lo)
+    u = rng.uniform(lo_v, hi_v, size=(hi - lo, TUNER_DRAWS_PER_CANDIDATE))
+    return u[:, 0:3].copy(), u[:, 3:6].copy(), u[:, 6:10].copy()
+
+
 def episode_masses(lo: int, hi: int, device) -> torch.Tensor:
     """default_rng(10**9 + i).uniform(0.8, 1.2) for i in [lo, hi), drawn on the
     device (qt_seed_uniform)."""
@@ -104,11 +116,8 @@ def build(config: int, lo: int | None = None, hi: int | None = None, device=None
     elif config == 3:
         ctl = BatchedRiccatiLQR(dict(LQI_CONFIG, dt=0.01), device=device)
     elif config == 4:
-        cands = tuner_candidates(lo, hi)
-        ctl = BatchedRiccatiLQR({"dt": 0.01}, device=device,
-                                q_pos=np.array([c["q_pos"] for c in cands]),
-                                q_vel=np.array([c["q_vel"] for c in cands]),
-                                r_controls=np.array([c["r_controls"] for c in cands]))
+        qp, qv, rc = tuner_candidate_arrays(lo, hi)
+        ctl = BatchedRiccatiLQR({"dt": 0.01}, device=device, q_pos=qp, q_vel=qv, r_controls=rc)
     else:
         motion = motion_of(lo, hi)
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -117,5 +126,6 @@ def build(config: int, lo: int | None = None, hi: int | None = None, device=None
     return Shard(config, lo, hi, ctl, env, seeds, motion, mass)
 
 
-__all__ = ["EPISODES", "MOTION", "LQI_CONFIG", "Shard", "shard_bounds", "tuner_candidates", "episode_masses",
+__all__ = ["EPISODES", "MOTION", "LQI_CONFIG", "Shard", "shard_bounds", "tuner_candidates", "tuner_candidate_arrays",
+           "episode_masses",
            "motion_of", "build"]

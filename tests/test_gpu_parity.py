@@ -156,6 +156,47 @@ def test_chunked_equals_single_launch(qt):
     assert torch.equal(a.state.x, b.state.x)
 
 
+@pytest.mark.parametrize("case", ["linear_lqr", "sinusoidal_lqi", "figure8_ff", "mixed_mass", "circular_tight"])
+def test_fast_path_equals_exact_path(qt, case):
+    """The branch-light fast step (taken when the wave qualifies and nothing is
+    recorded) against the exact step (forced by recording): the same decisions
+    (counts, codes, steps) and the same values up to rounding (the two code
+    paths are contracted into FMAs differently by the compiler)."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = 1024
+    env = {}
+    kw = {}
+    ctl_cfg = {"dt": 0.01}
+    if case == "linear_lqr":
+        env = {"target": {"motion_type": "linear"}}
+    elif case == "sinusoidal_lqi":
+        env = {"target": {"motion_type": "sinusoidal"}}
+        ctl_cfg.update(use_lqi=True, q_int=[1e-3, 1e-3, 1e-2])
+    elif case == "figure8_ff":
+        env = {"target": {"motion_type": "figure8"}}
+        ctl_cfg.update(feedforward_enabled=True, ff_velocity_gain=[0.1, 0.1, 0.1], ff_acceleration_gain=[0.05] * 3)
+    elif case == "mixed_mass":
+        kw = dict(motion=[i % 5 for i in range(n)], plant_mass=0.8 + 0.4 * np.arange(n) / n)
+    else:  # fast yaw/tilt motion: large gains drive the attitude to the clamps
+        env = {"target": {"motion_type": "circular", "speed": 4.0, "radius": 1.0}}
+        ctl_cfg.update(q_pos=[10.0, 10.0, 40.0], r_controls=[0.05, 0.05, 0.05, 0.05])
+    ctl = BatchedRiccatiLQR(ctl_cfg)
+    fast = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), **kw)
+    exact = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), record=True, **kw)
+    mf, me = fast.metrics.cpu().numpy(), exact.metrics.cpu().numpy()
+    discrete = ("overshoot_count", "success", "termination_code", "action_violations", "steps")
+    for i, f in enumerate(FIELDS):
+        if f in discrete:
+            np.testing.assert_array_equal(mf[i], me[i], err_msg=f)
+        else:
+            np.testing.assert_allclose(mf[i], me[i], rtol=1e-9, atol=1e-9, err_msg=f)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy(), exact.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(fast.state.integ.cpu().numpy(), exact.state.integ.cpu().numpy(), rtol=1e-9,
+                               atol=1e-9)
+
+
 def test_mixed_motion_order_permutation(qt):
     """Mixed motion types: the per-step runtime-motion kernel, the same kernel
     under a permuting `order`, and the grouped motion-specialised launches

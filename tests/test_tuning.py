@@ -89,3 +89,11 @@ def test_shard_bounds_partition():
             b = [workloads.shard_bounds(total, r, world) for r in range(world)]
             assert b[0][0] == 0 and b[-1][1] == total
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+
+
+def test_candidate_arrays_match_dicts():
+    qp, qv, rc = workloads.tuner_candidate_arrays(17, 400)
+    ref = workloads.tuner_candidates(17, 400)
+    assert qp.tolist() == [c["q_pos"] for c in ref]
+    assert qv.tolist() == [c["q_vel"] for c in ref]
+    assert rc.tolist() == [c["r_controls"] for c in ref]
