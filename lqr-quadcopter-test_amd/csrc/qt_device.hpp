@@ -175,9 +175,15 @@ struct Trig {
   double s[3], c[3];
 };
 
+// YAW0: the yaw angle and yaw rate are exactly zero for the whole launch (a
+// structured gain never commands yaw, u[3] = 0, so a yaw that starts at zero
+// stays zero: quadcopter_env.py:412-421 with u = 0, omega = 0).  Its sin / cos
+// are then exactly 0 / 1 and every yaw term drops out of the arithmetic.
+template <bool YAW0 = false>
 __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) fast_sincos(ang[i], &t.s[i], &t.c[i]);
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) fast_sincos(ang[i], &t.s[i], &t.c[i]);
+  if (YAW0) t.s[2] = 0.0, t.c[2] = 1.0;
 }
 
 // Trig of the RK4 stage angles  ang_i + delta_i  from the trig of ang_i:
@@ -185,12 +191,13 @@ __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 // with sin d / cos d from small_sincos.  The stage offsets are h * (body rate)
 // <= dt * ~12 rad/s; an offset beyond the polynomial's range takes fast_sincos.
 // SMALL: the caller has proven |delta| <= kSmallAngle (small_angle_bound).
-template <bool SMALL = false>
+template <bool SMALL = false, bool YAW0 = false>
 __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t) {
+  constexpr int NA = YAW0 ? 2 : 3;
   const double dm = SMALL ? 0.0 : fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
   if (SMALL || dm <= kSmallAngle) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < NA; ++i) {
       double sd, cd;
       small_sincos(delta[i], &sd, &cd);
       t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
@@ -198,16 +205,24 @@ __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, co
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) fast_sincos(ang[i] + delta[i], &t.s[i], &t.c[i]);
+    for (int i = 0; i < NA; ++i) fast_sincos(ang[i] + delta[i], &t.s[i], &t.c[i]);
   }
+  if (YAW0) t.s[2] = 0.0, t.c[2] = 1.0;
 }
 
+// _compute_derivatives (quadcopter_env.py:329-426).  Only the third column of
+// the ZYX rotation matrix multiplies the body thrust [0,0,T] (393).  Divisions
+// by mass and by the 0.1 s rate time constant are taken as multiplications by
+// reciprocals (<= 1 ulp per term; the closed loop is not chaotic).
+template <bool YAW0 = false>
 __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant& pl, const double* s,
                                             const double* u, const Trig& tr, double* d) {
   const double sphi = tr.s[0], cphi = tr.c[0], sth = tr.s[1], cth = tr.c[1], spsi = tr.s[2], cpsi = tr.c[2];
   const double T = u[0];
-  const double tw0 = (cpsi * sth * cphi + spsi * sphi) * T;
-  const double tw1 = (spsi * sth * cphi - cpsi * sphi) * T;
+  // with psi = 0: cpsi * a + spsi * b = a and spsi * a - cpsi * b = -b, exactly
+  // (up to the sign of a zero, which no later operation distinguishes)
+  const double tw0 = (YAW0 ? sth * cphi : cpsi * sth * cphi + spsi * sphi) * T;
+  const double tw1 = (YAW0 ? -sphi : spsi * sth * cphi - cpsi * sphi) * T;
   const double tw2 = (cth * cphi) * T;
   d[0] = s[3];
   d[1] = s[4];
@@ -217,21 +232,26 @@ __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant&
   d[5] = ((tw2 + pl.gz) + (-e.drag_linear * s[5])) * pl.inv_mass;
   d[6] = s[9];
   d[7] = s[10];
-  d[8] = s[11];
+  d[8] = YAW0 ? 0.0 : s[11];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) d[9 + i] = (u[1 + i] - s[9 + i]) * 10.0 - e.drag_angular * s[9 + i];
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) d[9 + i] = (u[1 + i] - s[9 + i]) * 10.0 - e.drag_angular * s[9 + i];
+  if (YAW0) d[11] = 0.0;
 }
 
 // _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held
 // constant across the four stages.
 // FAST: RK4 known (integrator == 0) and every stage offset proven small.
-template <bool FAST = false>
+// YAW0 (with FAST): yaw identically zero; x[8] and x[11] are left untouched.
+template <bool FAST = false, bool YAW0 = false>
 __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
+  static_assert(FAST || !YAW0, "YAW0 is a fast-path specialisation");
+  // state components that evolve (YAW0: all but yaw 8 and yaw rate 11)
+  auto live = [](int i) { return !YAW0 || (i != 8 && i != 11); };
   const double dt = e.dt;
   double k[12];
   Trig t0, ts;
-  trig_of(x + 6, t0);
-  derivatives(e, pl, x, u, t0, k);
+  trig_of<YAW0>(x + 6, t0);
+  derivatives<YAW0>(e, pl, x, u, t0, k);
   if (!FAST && e.integrator == 1) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
@@ -240,38 +260,43 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   // Stage states.  Their angles only enter through sin/cos (derivatives of
   // the angles are the body rates), so stage trig is the step-start trig
   // shifted by the stage offset h * k[6..8].
-  double acc[12], tmp[12], del[3];
+  double acc[12], tmp[12], del[3] = {0.0, 0.0, 0.0};
   const double h2 = 0.5 * dt;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
+    if (!live(i)) continue;
     acc[i] = k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
+  if (YAW0) tmp[8] = tmp[11] = 0.0;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
-  trig_shift<FAST>(x + 6, t0, del, ts);
-  derivatives(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = h2 * k[6 + i];
+  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
+  derivatives<YAW0>(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
+    if (!live(i)) continue;
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
-  trig_shift<FAST>(x + 6, t0, del, ts);
-  derivatives(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = h2 * k[6 + i];
+  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
+  derivatives<YAW0>(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
+    if (!live(i)) continue;
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + dt * k[i];
   }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) del[i] = dt * k[6 + i];
-  trig_shift<FAST>(x + 6, t0, del, ts);
-  derivatives(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = dt * k[6 + i];
+  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
+  derivatives<YAW0>(e, pl, tmp, u, ts, k);
   const double h6 = dt / 6.0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) x[i] = x[i] + h6 * (acc[i] + k[i]);
+  for (int i = 0; i < 12; ++i)
+    if (live(i)) x[i] = x[i] + h6 * (acc[i] + k[i]);
 }
 
 // Clip of a value known to be a number: one v_max + one v_min.  (IEEE maxNum
@@ -394,23 +419,25 @@ __host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ct
 // needed: speed within 1e-14 of the clamp or above it, or an attitude angle
 // with (a + pi) outside (-2 pi, 4 pi), where numpy's floor-mod takes more
 // than one correction (or the state is not finite).
+template <bool YAW0 = false>
 __device__ __forceinline__ bool constrain_fast_ok(const qt_env_params& e, const double* x) {
   const double sv = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
   const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
   bool ok = sv < vm2;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
     const double b = x[6 + i] + kPi;
     ok = ok & (b > -kTwoPi) & (b < 2.0 * kTwoPi);
   }
   return ok;
 }
 
+template <bool YAW0 = false>
 __device__ __forceinline__ void constrain_fast_apply(const qt_env_params& e, double* x) {
 #pragma unroll
-  for (int i = 9; i < 12; ++i) x[i] = clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+  for (int i = 9; i < (YAW0 ? 11 : 12); ++i) x[i] = clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
     // (b % 2 pi) for b in (-2 pi, 4 pi): one correction, the same rounding as
     // numpy's (b < 0: b + 2 pi; b >= 2 pi: b - 2 pi, exact by Sterbenz)
     const double b = x[6 + i] + kPi;

@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev
 // takes the exact step's decisions; rare lanes/steps (speed at the
 // clamp, attitude far outside [-pi, pi), tracking error at the radius within
 // 1e-14) fall back to the exact constraint / comparison code inside the step.
-template <bool FAST, int MOTION, int KC, bool FF, bool KS>
+template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
 __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
                                           const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
@@ -199,14 +199,14 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     // ---- env.step (quadcopter_env.py:152-232)
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
-      integrate<true>(e, pl, x, u);
+      integrate<true, YAW0>(e, pl, x, u);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
-      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok(e, x));
+      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
       if (ok) {
-        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply(e, x);
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
         a.on_post += se < er2lo;
       } else {  // rare: exact constraints and comparison
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
@@ -288,11 +288,17 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c) &&
                     __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
-  if (fast)
-    run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n, ep);
+  // structured gains never command yaw: a yaw at rest stays exactly zero
+  const bool yaw0 = KS && fast && __builtin_amdgcn_ballot_w64(!(x[8] == 0.0 && x[11] == 0.0)) == 0;
+  if (KS && yaw0)
+    run_steps<true, KS, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n,
+                                            ep);
+  else if (fast)
+    run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
+                                               n, ep);
   else
-    run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n,
-                                         ep);
+    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
+                                                n, ep);
 
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
