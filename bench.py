@@ -163,7 +163,8 @@ def main():
 
     if rank == 0:
         achieved = FLOPS_PER_ENV_STEP * local_env_steps / (kern_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic("rollout_kernel<1, 6, false, true>")
+        # the dominant kernel: the fast yaw-at-rest flavour (older profiles: the single-flavour kernel)
+        traffic, traffic_src = pmc_traffic(("rollout_kernel<2, 1, 6, false, true>", "rollout_kernel<1, 6, false, true>"))
         # algorithmic HBM bytes of one launch: per-episode state in (x 12, target 9, t, acc 14,
         # pattern 3 doubles) and out (x, target, t, acc); gains are a broadcast
         algo_bytes = (39 + 36) * 8 * n
@@ -189,7 +190,9 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": algo_bytes,
                          "hbm_GBps_achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3),
-                         "kernel": "rollout_kernel<LINEAR, K=6, no-FF, structured K>", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "rollout_kernel<yaw-at-rest fast step, LINEAR, K=6, no-FF, structured K> "
+                                   "+ its deferred exact pass (HIP events around both)",
+                         "kernel_ms": round(kern_ms, 4),
                          "flops_per_env_step": FLOPS_PER_ENV_STEP},
             "cpu_baseline": cpu,
             "tracking": track,
@@ -200,30 +203,30 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kernel_tag: str):
+def pmc_traffic(kernel_tags):
     """HBM bytes per rollout launch from the committed rocprofv3 PMC passes
-    (profiles/r*/pmc_FETCH_SIZE.csv, pmc_WRITE_SIZE.csv; scripts/profile_session.sh).
+    (profiles/r*/pmc_FETCH_SIZE.csv, pmc_WRITE_SIZE.csv; scripts/profile_session.sh),
+    newest profile first, first kernel tag that matches.
     gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
     (MI355X_MICROARCH.md §HBM), so it is doubled; both counters are in KiB."""
     import csv
     import glob
 
-    dirs = sorted(d for d in glob.glob(os.path.join(ROOT, "profiles", "r*"))
-                  if os.path.exists(os.path.join(d, "pmc_FETCH_SIZE.csv")))
-    if not dirs:
-        return None, None
+    dirs = sorted((d for d in glob.glob(os.path.join(ROOT, "profiles", "r*"))
+                   if os.path.exists(os.path.join(d, "pmc_FETCH_SIZE.csv"))), reverse=True)
 
-    def avg(path, counter):
+    def avg(path, counter, tag):
         vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if r["Counter_Name"] == counter and kernel_tag in r["Kernel_Name"]]
+                if r["Counter_Name"] == counter and tag in r["Kernel_Name"]]
         return sum(vals) / len(vals) if vals else None
 
-    d = dirs[-1]
-    f = avg(os.path.join(d, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE")
-    w = avg(os.path.join(d, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE")
-    if f is None or w is None:
-        return None, d
-    return (2.0 * f + w) * 1024.0, os.path.relpath(d, ROOT)
+    for d in dirs:
+        for tag in kernel_tags:
+            f = avg(os.path.join(d, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", tag)
+            w = avg(os.path.join(d, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", tag)
+            if f is not None and w is not None:
+                return (2.0 * f + w) * 1024.0, os.path.relpath(d, ROOT)
+    return None, None
 
 
 def cpu_baseline(args, cfg, seeds, gpu_met):

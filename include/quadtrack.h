@@ -274,6 +274,13 @@ int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, const double
    means of the first gives the population std (np.std) without cancellation. */
 int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, void* stream);
 
+/* qt_summary over `nparts` workgroups (1..4096): workgroup b reduces the
+   contiguous episodes [b*c, (b+1)*c), c = ceil(n / nparts), into work[b][11],
+   then one workgroup combines the parts in index order.  Same out[11];
+   bitwise reproducible for a given (n, nparts).  work: DEVICE [nparts * 11]. */
+int qt_summary_parts(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, double* work,
+                     int32_t nparts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -248,11 +248,14 @@ __device__ __forceinline__ bool all_finite(const double* v, int k) {
   return s == 0.0;
 }
 
+// step flavours: the exact step, the fast step, the fast step with yaw at rest
+constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
+
 // MOTION >= 0 specialises the target pattern; -1 reads it per episode.
-template <int MOTION, int KC, bool FF, bool KS>
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
-                                                         double* __restrict__ rec) {
+                                                         double* __restrict__ rec, int deferred) {
   const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (slot >= b.slot_end) return;
   const int64_t n = b.n, ep = episode_of(b, slot);
@@ -280,25 +283,28 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   double t = st.t[ep];
   Acc a = load_acc(st.acc, n, ep);
 
-  // fast path for the whole wavefront when every lane qualifies (uniform branch)
+  // Which step the wavefront runs (uniform).  A fast flavour is launched only
+  // when the launch-level preconditions hold (fast_path_ok, no recording); it
+  // takes the waves whose lanes all qualify and leaves the others untouched,
+  // and the exact kernel launched after it with `deferred` = that flavour
+  // takes exactly those (the same test on the same inputs).
   bool lane_ok = a.term != QT_TERM_RUNNING ||
                  (all_finite(G.k, Gains<KC, KS>::kCount) && all_finite(x, 12) && all_finite(integ, 3) &&
                   all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && isfinite(hover) &&
                   isfinite(pl.inv_mass) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
-  const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c) &&
-                    __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
   // structured gains never command yaw: a yaw at rest stays exactly zero
-  const bool yaw0 = KS && fast && __builtin_amdgcn_ballot_w64(!(x[8] == 0.0 && x[11] == 0.0)) == 0;
-  if (KS && yaw0)
-    run_steps<true, KS, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec, n,
-                                            ep);
-  else if (fast)
-    run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
-                                               n, ep);
-  else
+  if (FLAVOR == kYaw0 || deferred == kYaw0) lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0;
+  const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
+  if (FLAVOR != kExact) {
+    if (!wave_ok) return;
+    run_steps<true, FLAVOR == kYaw0, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a,
+                                                         nsteps, rec, n, ep);
+  } else {
+    if (deferred != kExact && wave_ok) return;
     run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
                                                 n, ep);
+  }
 
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
@@ -526,35 +532,53 @@ __global__ __launch_bounds__(kBlock) void metrics_arrays_kernel(qt_criteria cr, 
   for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
 }
 
-// EvaluationSummary partials (utils/metrics.py:341-390): one workgroup,
-// fixed summation order (bitwise reproducible), first-index argmax/argmin.
+// EvaluationSummary partials (utils/metrics.py:341-390): fixed summation
+// order (bitwise reproducible for a given n), first-index argmax/argmin.
+// Partial vector: [7 sums, max, argmax, min, argmin]; an argmax/argmin < 0
+// marks an empty partial.
 constexpr int kSumBlock = 256;
-__global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const double* __restrict__ met, double mu_r,
-                                                            double mu_e, double* out) {
+constexpr int kSumParts = 11;
+
+struct SumPart {
+  double s[7];
+  double vmax, vmin;
+  int64_t imax, imin;
+};
+
+__device__ __forceinline__ void sum_empty(SumPart& p) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) p.s[k] = 0.0;
+  p.vmax = -INFINITY, p.vmin = INFINITY, p.imax = -1, p.imin = -1;
+}
+
+// episodes [lo, hi) of met, strided over the block's threads
+__device__ __forceinline__ void sum_accumulate(SumPart& p, int64_t n, const double* __restrict__ met, double mu_r,
+                                               double mu_e, int64_t lo, int64_t hi) {
+  for (int64_t e = lo + threadIdx.x; e < hi; e += kSumBlock) {
+    const double r = met[QT_MET_ON_TARGET_RATIO * n + e], er = met[QT_MET_MEAN_ERR * n + e];
+    p.s[0] += r;
+    p.s[1] += er;
+    p.s[2] += met[QT_MET_MEAN_EFFORT * n + e];
+    p.s[3] += met[QT_MET_SUCCESS * n + e];
+    p.s[4] += 1.0;
+    p.s[5] += (r - mu_r) * (r - mu_r);
+    p.s[6] += (er - mu_e) * (er - mu_e);
+    if (r > p.vmax || p.imax < 0) p.vmax = r, p.imax = e;
+    if (r < p.vmin || p.imin < 0) p.vmin = r, p.imin = e;
+  }
+}
+
+// tree-combine every thread's partial (fixed pairing); thread 0 writes out[11]
+__device__ void sum_block_reduce(const SumPart& p, double* out) {
   __shared__ double sh[7][kSumBlock];
   __shared__ double shx[2][kSumBlock];
   __shared__ int64_t shi[2][kSumBlock];
-  double s[7] = {0, 0, 0, 0, 0, 0, 0};
-  double vmax = -INFINITY, vmin = INFINITY;
-  int64_t imax = -1, imin = -1;
-  for (int64_t e = threadIdx.x; e < n; e += kSumBlock) {
-    const double r = met[QT_MET_ON_TARGET_RATIO * n + e], er = met[QT_MET_MEAN_ERR * n + e];
-    s[0] += r;
-    s[1] += er;
-    s[2] += met[QT_MET_MEAN_EFFORT * n + e];
-    s[3] += met[QT_MET_SUCCESS * n + e];
-    s[4] += 1.0;
-    s[5] += (r - mu_r) * (r - mu_r);
-    s[6] += (er - mu_e) * (er - mu_e);
-    if (r > vmax || imax < 0) vmax = r, imax = e;
-    if (r < vmin || imin < 0) vmin = r, imin = e;
-  }
 #pragma unroll
-  for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] = s[k];
-  shx[0][threadIdx.x] = vmax;
-  shx[1][threadIdx.x] = vmin;
-  shi[0][threadIdx.x] = imax;
-  shi[1][threadIdx.x] = imin;
+  for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] = p.s[k];
+  shx[0][threadIdx.x] = p.vmax;
+  shx[1][threadIdx.x] = p.vmin;
+  shi[0][threadIdx.x] = p.imax;
+  shi[1][threadIdx.x] = p.imin;
   __syncthreads();
   for (int w = kSumBlock / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) {
@@ -583,6 +607,43 @@ __global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const dou
   }
 }
 
+// one workgroup over all episodes
+__global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const double* __restrict__ met, double mu_r,
+                                                            double mu_e, double* out) {
+  SumPart p;
+  sum_empty(p);
+  sum_accumulate(p, n, met, mu_r, mu_e, 0, n);
+  sum_block_reduce(p, out);
+}
+
+// stage 1 of the multi-workgroup form: workgroup b reduces episodes
+// [b * chunk, (b + 1) * chunk) into part[b][11]
+__global__ __launch_bounds__(kSumBlock) void summary_part_kernel(int64_t n, const double* __restrict__ met,
+                                                                 double mu_r, double mu_e, int64_t chunk,
+                                                                 double* part) {
+  SumPart p;
+  sum_empty(p);
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  sum_accumulate(p, n, met, mu_r, mu_e, lo, lo + chunk < n ? lo + chunk : n);
+  sum_block_reduce(p, part + (int64_t)blockIdx.x * kSumParts);
+}
+
+// stage 2: one workgroup combines the nparts partials in a fixed order
+__global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, const double* __restrict__ part,
+                                                                  double* out) {
+  SumPart p;
+  sum_empty(p);
+  for (int j = threadIdx.x; j < nparts; j += kSumBlock) {
+    const double* q = part + (int64_t)j * kSumParts;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) p.s[k] += q[k];
+    const int64_t ia = (int64_t)q[8], ja = (int64_t)q[10];
+    if (ia >= 0 && (p.imax < 0 || q[7] > p.vmax || (q[7] == p.vmax && ia < p.imax))) p.vmax = q[7], p.imax = ia;
+    if (ja >= 0 && (p.imin < 0 || q[9] < p.vmin || (q[9] == p.vmin && ja < p.imin))) p.vmin = q[9], p.imin = ja;
+  }
+  sum_block_reduce(p, out);
+}
+
 BatchDev to_dev(const qt_batch* b) {
   return BatchDev{b->n, b->motion, b->pattern, b->plant_mass, b->hover_thrust, b->K, b->k_per_episode, b->order,
                   0, b->n};
@@ -592,27 +653,40 @@ int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
 
 int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
 
+template <int MOTION, int KC, bool FF, bool KS>
+void launch_flavours(bool fast, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                     const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
+  constexpr int kF = KS ? kYaw0 : kFast;
+  if (fast) {
+    rollout_kernel<kF, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kF);
+  } else {
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
+  }
+}
+
 template <int KC, bool FF, bool KS>
-void launch_rollout_motion(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
-                           const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
+void launch_rollout_motion(int motion, bool fast, int grid, hipStream_t s, const qt_env_params& e,
+                           const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st,
+                           int nsteps, double* rec) {
   switch (motion) {
     case QT_MOTION_STATIONARY:
-      rollout_kernel<QT_MOTION_STATIONARY, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_STATIONARY, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_LINEAR:
-      rollout_kernel<QT_MOTION_LINEAR, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_LINEAR, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_CIRCULAR:
-      rollout_kernel<QT_MOTION_CIRCULAR, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_CIRCULAR, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_SINUSOIDAL:
-      rollout_kernel<QT_MOTION_SINUSOIDAL, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_SINUSOIDAL, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_FIGURE8:
-      rollout_kernel<QT_MOTION_FIGURE8, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_FIGURE8, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     default:
-      rollout_kernel<-1, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec);
+      launch_flavours<-1, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
   }
 }
 
@@ -620,16 +694,17 @@ template <int KC>
 void launch_rollout(bool ff, bool ks, int motion, int grid, hipStream_t s, const qt_env_params& e,
                     const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                     double* rec) {
+  const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
   if (ff) {
     if (ks)
-      launch_rollout_motion<KC, true, true>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, true, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
     else
-      launch_rollout_motion<KC, true, false>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, true, false>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
   } else {
     if (ks)
-      launch_rollout_motion<KC, false, true>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, false, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
     else
-      launch_rollout_motion<KC, false, false>(motion, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, false, false>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
   }
 }
 
@@ -753,6 +828,16 @@ int qt_metrics_from_arrays(const qt_criteria* crit, int64_t n, int32_t max_steps
 int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, void* stream) {
   if (!met || !out || n < 0) return QT_EINVAL;
   summary_kernel<<<1, kSumBlock, 0, (hipStream_t)stream>>>(n, met, mu_ratio, mu_err, out);
+  return check_launch();
+}
+
+int qt_summary_parts(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, double* work,
+                     int32_t nparts, void* stream) {
+  if (!met || !out || !work || n < 0 || nparts < 1 || nparts > 4096) return QT_EINVAL;
+  const int64_t chunk = (n + nparts - 1) / nparts > 0 ? (n + nparts - 1) / nparts : 1;
+  hipStream_t s = (hipStream_t)stream;
+  summary_part_kernel<<<nparts, kSumBlock, 0, s>>>(n, met, mu_ratio, mu_err, chunk, work);
+  summary_final_kernel<<<1, kSumBlock, 0, s>>>(nparts, work, out);
   return check_launch();
 }
 

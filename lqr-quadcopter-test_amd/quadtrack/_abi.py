@@ -81,7 +81,8 @@ class State(C.Structure):
 
 EXPORTS = ("qt_abi_version", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_grouped",
            "qt_env_step", "qt_compute_action", "qt_target_state",
-           "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary")
+           "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary",
+           "qt_summary_parts")
 
 _lib = None
 
@@ -115,6 +116,7 @@ def load():
     L.qt_dare_batched.argtypes = [i32, i64, dbl, dbl, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     L.qt_dare_dense.argtypes = [i32, i32, i64, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
     L.qt_summary.argtypes = [i64, vp, dbl, dbl, vp, vp]
+    L.qt_summary_parts.argtypes = [i64, vp, dbl, dbl, vp, vp, i32, vp]
     for name in EXPORTS[1:]:
         getattr(L, name).restype = C.c_int
     v = L.qt_abi_version()

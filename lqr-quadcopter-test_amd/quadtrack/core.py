@@ -212,13 +212,26 @@ def episode_metrics(crit: Criteria, st: RolloutState) -> torch.Tensor:
     return met
 
 
-def summary_partials(met: torch.Tensor, mu_ratio=0.0, mu_err=0.0) -> torch.Tensor:
-    """[sum ratio, sum err, sum effort, sum success, count, M2 ratio, M2 err, max, argmax, min, argmin]."""
+def summary_parts_for(n: int) -> int:
+    """Workgroups of the summary reduction: ~1,024 episodes each, at most 1,024."""
+    return max(1, min(1024, -(-n // 1024)))
+
+
+def summary_partials(met: torch.Tensor, mu_ratio=0.0, mu_err=0.0, nparts: int | None = None) -> torch.Tensor:
+    """[sum ratio, sum err, sum effort, sum success, count, M2 ratio, M2 err, max, argmax, min, argmin]
+    (qt_summary_parts; nparts = 1 is the single-workgroup qt_summary)."""
     lib = _abi.load()
+    n = met.shape[1]
+    nparts = summary_parts_for(n) if nparts is None else int(nparts)
     out = torch.zeros(11, dtype=F64, device=met.device)
     with torch.cuda.device(met.device):
-        check(lib.qt_summary(met.shape[1], ptr(met), float(mu_ratio), float(mu_err), ptr(out),
-                             stream_of(met.device)), "qt_summary")
+        if nparts == 1:
+            check(lib.qt_summary(n, ptr(met), float(mu_ratio), float(mu_err), ptr(out), stream_of(met.device)),
+                  "qt_summary")
+        else:
+            work = torch.empty(nparts * 11, dtype=F64, device=met.device)
+            check(lib.qt_summary_parts(n, ptr(met), float(mu_ratio), float(mu_err), ptr(out), ptr(work), nparts,
+                                       stream_of(met.device)), "qt_summary_parts")
     return out
 
 

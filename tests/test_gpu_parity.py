@@ -458,6 +458,34 @@ def test_episode_metrics_and_summary(qt):
     assert M.compute_episode_metrics([]).termination_reason == "no_data"
 
 
+@pytest.mark.parametrize("nparts", [1, 7, 64, 1024])
+def test_summary_partials_multiblock(qt, nparts):
+    """qt_summary / qt_summary_parts against numpy on 100,003 episodes with
+    tied on-target ratios (first-occurrence argmax/argmin), and run-to-run
+    bitwise determinism."""
+    from quadtrack import core
+    from quadtrack._abi import MET, MET_ROWS
+
+    n = 100003
+    rng = np.random.default_rng(5)
+    met = np.zeros((MET_ROWS, n))
+    ratio = rng.integers(0, 3001, n) / 3000.0
+    met[MET["on_target_ratio"]] = ratio
+    met[MET["mean_tracking_error"]] = rng.lognormal(size=n)
+    met[MET["mean_control_effort"]] = rng.uniform(5, 15, n)
+    met[MET["success"]] = rng.integers(0, 2, n)
+    t = torch.as_tensor(met, device="cuda")
+    a = core.summary_partials(t, 0.3, 1.1, nparts=nparts).cpu().numpy()
+    b = core.summary_partials(t, 0.3, 1.1, nparts=nparts).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    er = met[MET["mean_tracking_error"]]
+    ref = [ratio.sum(), er.sum(), met[MET["mean_control_effort"]].sum(), met[MET["success"]].sum(), n,
+           ((ratio - 0.3) ** 2).sum(), ((er - 1.1) ** 2).sum()]
+    np.testing.assert_allclose(a[:7], ref, rtol=1e-12)
+    assert a[7] == ratio.max() and int(a[8]) == int(np.argmax(ratio))
+    assert a[9] == ratio.min() and int(a[10]) == int(np.argmin(ratio))
+
+
 def test_evaluate_batched_vs_evaluator(qt):
     """Batched evaluator == the drop-in sequential Evaluator for LQR (no
     integral, so the carry-over of SURVEY F8 is moot)."""
