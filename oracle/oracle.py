@@ -77,6 +77,7 @@ def lib():
         L.oq_env_step.restype = C.c_int
         L.oq_compute_action.argtypes = [P(CtrlParams), dp, C.c_int, C.c_double, dp, dp, dp]
         L.oq_compute_action.restype = C.c_int
+        L.oq_compute_action_pid.argtypes = [P(CtrlParams), dp, C.c_double, dp, dp, dp, dp]
         L.oq_episode.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), C.c_int, dp, C.c_double, C.c_double,
                                  dp, C.c_int, dp, C.c_int, dp, dp, dp, dp]
         L.oq_rollout.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), C.c_long, P(C.c_int8), dp, dp, dp,
@@ -153,10 +154,74 @@ def _vec3(v):
     return [float(v)] * 3 if np.isscalar(v) else [float(x) for x in v]
 
 
+def _base_params(cfg: dict, integral_limit_default: float) -> CtrlParams:
+    """Output clamps and feed-forward options shared by the three controllers."""
+    c = CtrlParams()
+    c.dt = cfg.get("dt", 0.01)
+    c.hover_thrust = cfg.get("mass", 1.0) * cfg.get("gravity", 9.81)
+    c.min_thrust = cfg.get("min_thrust", 0.0)
+    c.max_thrust = cfg.get("max_thrust", 20.0)
+    c.max_rate = cfg.get("max_rate", 3.0)
+    c.use_lqi = 0
+    c.feedforward_enabled = int(bool(cfg.get("feedforward_enabled", False)))
+    c.integral_limit = cfg.get("integral_limit", integral_limit_default)
+    c.integral_zero_threshold = cfg.get("integral_zero_threshold", 0.01)
+    fv, fa = _vec3(cfg.get("ff_velocity_gain", 0.0)), _vec3(cfg.get("ff_acceleration_gain", 0.0))
+    for i in range(3):
+        c.ff_velocity_gain[i] = fv[i]
+        c.ff_acceleration_gain[i] = fa[i]
+    c.ff_max_velocity = cfg.get("ff_max_velocity", 10.0)
+    c.ff_max_acceleration = cfg.get("ff_max_acceleration", 5.0)
+    return c
+
+
+def pid_controller(cfg: dict | None = None):
+    """PIDController.__init__ (controllers/__init__.py:158-241): (CtrlParams,
+    gains [kp, ki, kd] 3 x 3, kcols = 3)."""
+    cfg = dict(cfg or {})
+    c = _base_params(cfg, 0.0)
+    kp = _vec3(cfg.get("kp_pos", cfg.get("kp", [0.01, 0.01, 4.0])))
+    ki = _vec3(cfg.get("ki_pos", cfg.get("ki", [0.0, 0.0, 0.0])))
+    kd = _vec3(cfg.get("kd_pos", cfg.get("kd", [0.06, 0.06, 2.0])))
+    return c, np.array([kp, ki, kd], dtype=float), 3
+
+
+def lqr_controller(cfg: dict | None = None):
+    """LQRController.__init__ (controllers/__init__.py:449-574): heuristic or
+    given K, no integral: (CtrlParams, K 4 x 6, kcols = 6)."""
+    cfg = dict(cfg or {})
+    c = _base_params(cfg, 0.0)
+    if cfg.get("K") is not None:
+        K = np.array(cfg["K"], dtype=float)
+    else:
+        K = heuristic_gains(cfg.get("q_pos", [1e-4, 1e-4, 16.0]), cfg.get("q_vel", [0.0036, 0.0036, 4.0]),
+                            cfg.get("r_thrust", 1.0), cfg.get("r_rate", 1.0))
+    return c, K, 6
+
+
+def compute_action_pid(c: CtrlParams, gains, obs16, state):
+    """state: integral[3] + last time (NaN = None); returns (u, state, diag[18])."""
+    state = _f64(state).copy()
+    u = np.zeros(4)
+    diag = np.zeros(18)
+    lib().oq_compute_action_pid(C.byref(c), _dp(_f64(gains)), c.hover_thrust, _dp(_f64(obs16)), _dp(state),
+                                _dp(u), _dp(diag))
+    return u, state, diag
+
+
 def controller(cfg: dict | None = None):
     """RiccatiLQRController.__init__ (riccati_lqr.py:418-535): returns
-    (CtrlParams, K 4 x kcols, kcols, fallback_flag, P)."""
+    (CtrlParams, K 4 x kcols, kcols, fallback_flag, P).  cfg["controller"]
+    "pid" / "lqr" selects PIDController / LQRController (K = their gains,
+    kcols 3 / 6, no fallback, P None)."""
     cfg = dict(cfg or {})
+    kind = cfg.pop("controller", "riccati_lqr")
+    if kind == "pid":
+        c, K, kc = pid_controller(cfg)
+        return c, K, kc, False, None
+    if kind == "lqr":
+        c, K, kc = lqr_controller(cfg)
+        return c, K, kc, False, None
     mass = cfg.get("mass", 1.0)
     g = cfg.get("gravity", 9.81)
     dt = cfg.get("dt", 0.01)
@@ -322,5 +387,5 @@ def rollout(e, c, cr, motion, pat, mass, hover, K, kcols, k_per_episode, x0, max
         C.byref(e), C.byref(c), C.byref(cr), n, mo.ctypes.data_as(C.POINTER(C.c_int8)) if mo is not None else None,
         _dp(_f64(pat)), _dp(_f64(mass)) if mass is not None else None,
         _dp(_f64(hover)) if hover is not None else None, _dp(_f64(K)), kcols,
-        (4 * kcols) if k_per_episode else 0, _dp(_f64(x0)), int(max_steps), _dp(met), _dp(xf), _dp(integ))
+        (9 if kcols == 3 else 4 * kcols) if k_per_episode else 0, _dp(_f64(x0)), int(max_steps), _dp(met), _dp(xf), _dp(integ))
     return met, xf, integ, used

@@ -291,6 +291,68 @@ int oq_compute_action(const qt_ctrl_params* c, const double* K, int kcols, doubl
   return sat;
 }
 
+/* PIDController.compute_action (controllers/__init__.py:243-379).
+   gains: kp[3], ki[3], kd[3].  obs16: obs15 + observation time.
+   state: integral error[3], last observation time (NaN = None).
+   diag (optional, 18): p, i, d, ff_velocity, ff_acceleration, total correction. */
+void oq_compute_action_pid(const qt_ctrl_params* c, const double* gains, double hover, const double* obs16,
+                           double* state, double* u_out, double* diag) {
+  const double* kp = gains;
+  const double* ki = gains + 3;
+  const double* kd = gains + 6;
+  const double* qp = obs16;
+  const double* qv = obs16 + 3;
+  const double* tp = obs16 + 6;
+  const double* tv = obs16 + 9;
+  const double* ta = obs16 + 12;
+  const double now = obs16[15];
+  double ep[3];
+  for (int i = 0; i < 3; ++i) ep[i] = tp[i] - qp[i];
+  const double dt = isnan(state[3]) ? 0.0 : now - state[3]; /* 263-265 */
+  state[3] = now;
+  if (dt > 0) {
+    for (int i = 0; i < 3; ++i) state[i] += ep[i] * dt;
+    for (int i = 0; i < 3; ++i) state[i] = clipd(state[i], -c->integral_limit, c->integral_limit);
+  }
+  double p[3], it[3], etv[3] = {tv[0], tv[1], tv[2]}, ffv[3] = {0, 0, 0}, ffa[3] = {0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    p[i] = kp[i] * ep[i];
+    it[i] = ki[i] * state[i];
+  }
+  if (c->feedforward_enabled) {
+    double vm = norm3(etv);
+    if (vm > c->ff_max_velocity && vm > 0) {
+      double scl = c->ff_max_velocity / vm;
+      for (int i = 0; i < 3; ++i) etv[i] = etv[i] * scl;
+    }
+    for (int i = 0; i < 3; ++i) etv[i] = (1.0 + c->ff_velocity_gain[i]) * etv[i];
+    for (int i = 0; i < 3; ++i) ffv[i] = kd[i] * c->ff_velocity_gain[i] * etv[i] / (1.0 + c->ff_velocity_gain[i]);
+    double acc[3] = {ta[0], ta[1], ta[2]};
+    double am = norm3(acc);
+    if (am > c->ff_max_acceleration && am > 0)
+      for (int i = 0; i < 3; ++i) acc[i] = acc[i] / am * c->ff_max_acceleration;
+    for (int i = 0; i < 3; ++i) ffa[i] = c->ff_acceleration_gain[i] * acc[i];
+  }
+  double d[3], corr[3];
+  for (int i = 0; i < 3; ++i) {
+    d[i] = kd[i] * (etv[i] - qv[i]);
+    corr[i] = ((p[i] + it[i]) + d[i]) + ffa[i];
+  }
+  u_out[0] = clipd(hover + corr[2], c->min_thrust, c->max_thrust);
+  u_out[1] = clipd(-corr[1], -c->max_rate, c->max_rate);
+  u_out[2] = clipd(corr[0], -c->max_rate, c->max_rate);
+  u_out[3] = 0.0;
+  if (diag)
+    for (int i = 0; i < 3; ++i) {
+      diag[i] = p[i];
+      diag[3 + i] = it[i];
+      diag[6 + i] = d[i];
+      diag[9 + i] = ffv[i];
+      diag[12 + i] = ffa[i];
+      diag[15 + i] = corr[i];
+    }
+}
+
 /* ----------------------------------------------------------- closed loop */
 
 /* Evaluator.run_episode with a fresh controller (eval.py:95-167), per-episode
@@ -300,7 +362,7 @@ int oq_compute_action(const qt_ctrl_params* c, const double* K, int kcols, doubl
 void oq_episode(const qt_env_params* e, const qt_ctrl_params* c, const qt_criteria* cr, int motion,
                 const double* pat, double mass, double hover, const double* K, int kcols, const double* x0,
                 int max_steps, double* met, double* xf, double* integ_out, double* rec) {
-  double x[12], integ[3] = {0, 0, 0}, tgt[9], t = 0.0;
+  double x[12], integ[4] = {0, 0, 0, NAN}, tgt[9], t = 0.0; /* PID: integ[3] = last time */
   memcpy(x, x0, sizeof(x));
   oq_target_state(e, motion, pat, 0.0, tgt);
   double sum_e = 0, sum_e2 = 0, max_e = -INFINITY, sum_u = 0;
@@ -318,7 +380,14 @@ void oq_episode(const qt_env_params* e, const qt_ctrl_params* c, const qt_criter
     }
     for (int i = 0; i < 9; ++i) obs[6 + i] = tgt[i];
     double u[4];
-    oq_compute_action(c, K, kcols, hover, obs, integ, u);
+    if (kcols == 3) { /* PID: K holds kp, ki, kd */
+      double obs16[16];
+      memcpy(obs16, obs, sizeof(obs));
+      obs16[15] = t;
+      oq_compute_action_pid(c, K, hover, obs16, integ, u, NULL);
+    } else {
+      oq_compute_action(c, K, kcols, hover, obs, integ, u);
+    }
     /* pre-step record (eval.py:142-159) */
     double d[3] = {tgt[0] - x[0], tgt[1] - x[1], tgt[2] - x[2]};
     double ep = norm3(d);
@@ -370,7 +439,7 @@ void oq_episode(const qt_env_params* e, const qt_ctrl_params* c, const qt_criter
   if (steps == 0) { /* compute_episode_metrics on no data (metrics.py:287-291) */
     memset(met, 0, sizeof(double) * QT_MET_ROWS);
     memcpy(xf, x, sizeof(x));
-    memcpy(integ_out, integ, sizeof(integ));
+    memcpy(integ_out, integ, 3 * sizeof(double));
     return;
   }
   double ns = (double)steps;
@@ -390,7 +459,7 @@ void oq_episode(const qt_env_params* e, const qt_ctrl_params* c, const qt_criter
   met[QT_MET_ENV_ON_TARGET_RATIO] = steps ? (double)on_post / ns : 0.0;
   met[QT_MET_STEPS] = ns;
   memcpy(xf, x, sizeof(x));
-  memcpy(integ_out, integ, sizeof(integ));
+  memcpy(integ_out, integ, 3 * sizeof(double));
 }
 
 /* Many episodes (AoS inputs, stride per episode), OpenMP over episodes.

@@ -17,7 +17,9 @@ Fixture files (all float64 unless noted):
   target_states.npz   TargetMotion.get_state(t) (target_motion.py:29-411)
   actions.npz         RiccatiLQRController.compute_action on observation
                       sequences (riccati_lqr.py:779-967)
-  open_loop.npz       QuadcopterEnv.step under fixed action sequences
+  controller_actions.npz  PIDController / LQRController.compute_action with
+                      observation times (controllers/__init__.py:116-700)
+  open_loop.npz      QuadcopterEnv.step under fixed action sequences
                       (quadcopter_env.py:152-465)
   closed_loop.npz     closed-loop episodes: selected-step states/actions and
                       per-episode metrics (eval.py:95-167, utils/metrics.py:264-338)
@@ -278,6 +280,70 @@ def gen_actions(qt):
     return out
 
 
+CONTROLLER_CASES = [
+    {"controller": "pid"},
+    {"controller": "pid", "kp_pos": 0.5, "ki_pos": [0.1, 0.2, 0.3], "kd_pos": [0.1, 0.1, 1.0],
+     "integral_limit": 0.05},
+    {"controller": "pid", "ki_pos": [0.05, 0.05, 0.5], "integral_limit": 2.0, "feedforward_enabled": True,
+     "ff_velocity_gain": [0.5, 0.5, 0.2], "ff_acceleration_gain": 0.4, "ff_max_velocity": 1.0,
+     "ff_max_acceleration": 0.7, "mass": 1.4, "max_rate": 0.5},
+    {"controller": "lqr"},
+    {"controller": "lqr", "q_pos": [1e-3, 2e-3, 9.0], "r_thrust": 2.0, "r_rate": 0.25,
+     "feedforward_enabled": True, "ff_velocity_gain": 0.3, "ff_acceleration_gain": [0.2, 0.3, 0.4]},
+    {"controller": "lqr", "K": [[0.0, 0.1, 3.0, 0.0, 0.2, 2.0], [0.05, -0.3, 0.0, 0.1, -0.6, 0.0],
+                                [0.3, 0.02, 0.0, 0.7, 0.0, 0.01], [0.01, 0.01, 0.0, 0.0, 0.0, 0.02]]},
+]
+
+
+def gen_controller_actions(qt):
+    """PIDController / LQRController.compute_action (controllers/__init__.py:243-396, 576-700)
+    on an observation sequence with a `time` entry (the PID integrates over
+    time differences; a repeated and a decreasing time are included)."""
+    rng = np.random.default_rng(78)
+    T = 150
+    obs_arr = np.zeros((T, 15))
+    times = np.zeros(T)
+    base = rng.normal(size=15)
+    t = 0.0
+    for k in range(T):
+        base = base + 0.05 * rng.normal(size=15)
+        if k % 41 == 7:
+            base[6:9] += rng.normal(size=3) * 6.0
+        obs_arr[k] = base
+        obs_arr[k, 2] += 1.0
+        if k == 60:
+            pass  # repeated time: dt = 0
+        elif k == 100:
+            t = 0.37  # time going backwards: dt < 0
+        elif k > 0:
+            t += 0.01
+        times[k] = t
+    out = {"obs": obs_arr, "time": times}
+    for ci, c in enumerate(CONTROLLER_CASES):
+        ctl = make_controller(c)
+        A = np.zeros((T, 4))
+        I = np.zeros((T, 3))
+        for k in range(T):
+            o = obs_arr[k]
+            obs = {
+                "quadcopter": {"position": o[0:3].copy(), "velocity": o[3:6].copy(),
+                               "attitude": np.zeros(3), "angular_velocity": np.zeros(3)},
+                "target": {"position": o[6:9].copy(), "velocity": o[9:12].copy(),
+                           "acceleration": o[12:15].copy()},
+                "time": float(times[k]),
+            }
+            a = ctl.compute_action(obs)
+            A[k] = [a["thrust"], a["roll_rate"], a["pitch_rate"], a["yaw_rate"]]
+            if hasattr(ctl, "integral_error"):
+                I[k] = ctl.integral_error
+        out[f"case{ci}_action"] = A
+        out[f"case{ci}_integral"] = I
+        if c["controller"] == "lqr":
+            out[f"case{ci}_K"] = np.array(ctl.K)
+    out["cases_json"] = np.array(json.dumps(CONTROLLER_CASES))
+    return out
+
+
 # --------------------------------------------------------------------------- open loop
 
 
@@ -335,15 +401,24 @@ def gen_open_loop(qt):
 REC_STEPS = np.unique(np.concatenate([np.arange(0, 50), np.arange(0, 3000, 100), np.arange(2950, 3000)]))
 
 
+def make_controller(ctl_cfg):
+    """controller kind from the scenario's "controller" key (default riccati_lqr)."""
+    from quadcopter_tracking.controllers import LQRController, PIDController
+    from quadcopter_tracking.controllers.riccati_lqr import RiccatiLQRController
+
+    cfg = dict(ctl_cfg)
+    kind = cfg.pop("controller", "riccati_lqr")
+    return {"riccati_lqr": RiccatiLQRController, "pid": PIDController, "lqr": LQRController}[kind](config=cfg)
+
+
 def run_episode(qt, env_cfg, ctl_cfg, seed):
     """Evaluator.run_episode semantics (eval.py:95-167) with a fresh controller
     per episode.  Returns the recorded per-step arrays and metrics."""
-    from quadcopter_tracking.controllers.riccati_lqr import RiccatiLQRController
     from quadcopter_tracking.env import QuadcopterEnv
     from quadcopter_tracking.utils.metrics import compute_episode_metrics
 
     env = QuadcopterEnv(env_cfg)
-    ctl = RiccatiLQRController(config=dict(ctl_cfg))
+    ctl = make_controller(ctl_cfg)
     obs = env.reset(seed=seed)
     x0 = env.get_state_vector()
     data, states, acts, ints = [], [], [], []
@@ -360,8 +435,11 @@ def run_episode(qt, env_cfg, ctl_cfg, seed):
         })
         states.append(env.get_state_vector())
         acts.append(data[-1]["action"])
-        st = ctl.get_integral_state()
-        ints.append(st if st is not None else np.zeros(3))
+        if hasattr(ctl, "get_integral_state"):
+            st = ctl.get_integral_state()
+        else:  # PID integral error (controllers/__init__.py:229)
+            st = getattr(ctl, "integral_error", None)
+        ints.append(np.array(st) if st is not None else np.zeros(3))
         obs = nobs
     m = compute_episode_metrics(data, None, info)
     met = np.array([
@@ -429,6 +507,32 @@ def closed_loop_scenarios():
                                                                     "min_episode_duration": 10.0}},
                "ctl": {"dt": 0.01, "mass": 1.2, "max_thrust": 30.0, "q_pos": [1e-3, 1e-3, 20.0]},
                "seeds": [6, 7], "record": False})
+    # PID and heuristic-LQR controllers in the same loop
+    pid = {"controller": "pid"}
+    for m in MOTIONS:
+        sc.append({"name": f"pid_{m}", "env": {"target": {"motion_type": m}}, "ctl": pid,
+                   "seeds": [0, 1, 42], "record": m in ("linear", "circular")})
+    sc.append({"name": "pid_integral_sinusoidal", "env": {"target": {"motion_type": "sinusoidal"}},
+               "ctl": {"controller": "pid", "kp_pos": [0.02, 0.02, 5.0], "ki_pos": [0.005, 0.005, 0.8],
+                       "kd_pos": [0.08, 0.08, 2.5], "integral_limit": 1.5},
+               "seeds": [0, 5], "record": True})
+    sc.append({"name": "pid_ff_circular", "env": {"target": {"motion_type": "circular", "speed": 3.0}},
+               "ctl": {"controller": "pid", "feedforward_enabled": True, "ff_velocity_gain": [0.3, 0.3, 0.1],
+                       "ff_acceleration_gain": [0.2, 0.2, 0.4], "ff_max_velocity": 2.5,
+                       "ff_max_acceleration": 1.0, "ki_pos": 0.01, "integral_limit": 0.5},
+               "seeds": [1, 2], "record": True})
+    sc.append({"name": "pid_saturating_linear", "env": {"target": {"motion_type": "linear", "speed": 4.0}},
+               "ctl": {"controller": "pid", "kp_pos": [2.0, 2.0, 30.0], "kd_pos": [1.0, 1.0, 10.0],
+                       "max_thrust": 18.0, "max_rate": 2.0},
+               "seeds": [3], "record": True})
+    for m in ("stationary", "linear", "circular"):
+        sc.append({"name": f"lqr_heuristic_{m}", "env": {"target": {"motion_type": m}},
+                   "ctl": {"controller": "lqr"}, "seeds": [0, 7], "record": m == "circular"})
+    sc.append({"name": "lqr_heuristic_custom_ff", "env": {"target": {"motion_type": "sinusoidal"}},
+               "ctl": {"controller": "lqr", "q_pos": [2e-4, 3e-4, 20.0], "q_vel": [5e-3, 4e-3, 5.0],
+                       "r_thrust": 0.8, "r_rate": 1.5, "feedforward_enabled": True,
+                       "ff_velocity_gain": 0.2, "ff_acceleration_gain": [0.1, 0.1, 0.3]},
+               "seeds": [2, 9], "record": False})
     return sc
 
 
@@ -481,6 +585,7 @@ def main():
     np.savez_compressed(os.path.join(args.out, "target_states.npz"), **gen_targets(qt))
     print("targets done", flush=True)
     np.savez_compressed(os.path.join(args.out, "actions.npz"), **gen_actions(qt))
+    np.savez_compressed(os.path.join(args.out, "controller_actions.npz"), **gen_controller_actions(qt))
     print("actions done", flush=True)
     np.savez_compressed(os.path.join(args.out, "open_loop.npz"), **gen_open_loop(qt))
     print("open loop done", flush=True)

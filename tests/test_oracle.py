@@ -136,6 +136,26 @@ def test_compute_action_sequences():
                 np.testing.assert_allclose(integ, A[f"case{ci}_integral"][k], rtol=1e-12, atol=1e-14)
 
 
+def test_pid_and_heuristic_lqr_action_sequences():
+    """PIDController / LQRController.compute_action (controllers/__init__.py)
+    over an observation sequence with times (repeated and decreasing ones)."""
+    A = np.load(os.path.join(GOLDEN, "controller_actions.npz"))
+    cases = json.loads(str(A["cases_json"]))
+    for ci, cfg in enumerate(cases):
+        c, K, kc, _, _ = O.controller(cfg)
+        if kc == 6:
+            np.testing.assert_allclose(K, A[f"case{ci}_K"], rtol=1e-15)
+        state = np.array([0.0, 0.0, 0.0, np.nan])
+        for k, obs in enumerate(A["obs"]):
+            if kc == 3:
+                u, state, _ = O.compute_action_pid(c, K, np.append(obs, A["time"][k]), state)
+                np.testing.assert_allclose(state[:3], A[f"case{ci}_integral"][k], rtol=1e-13, atol=1e-15)
+            else:
+                u, _, _ = O.compute_action(c, K, kc, obs, np.zeros(3))
+            np.testing.assert_allclose(u, A[f"case{ci}_action"][k], rtol=1e-12, atol=1e-12,
+                                       err_msg=f"case {ci} k {k}")
+
+
 def test_lqi_integral_known_answer():
     """The reference's one-step integral test (test_env_dynamics.py:3745-3785)."""
     c, K, kc, _, _ = O.controller({"dt": 0.01, "use_lqi": True, "q_int": [0.01, 0.01, 0.1], "integral_limit": 10.0})
