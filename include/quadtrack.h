@@ -14,11 +14,17 @@
  * Layout conventions (HBM, FP64, structure-of-arrays):
  *   state  x[12][n]   rows: px py pz vx vy vz roll pitch yaw p q r
  *                     (quadcopter_env.py:63-70)
- *   aux    integ[3][n] LQI integral state (riccati_lqr.py:484-486)
+ *   aux    integ[4][n] controller state: LQI integral (rows 0-2, riccati_lqr.py:484-486) or
+ *                     PID integral error (rows 0-2) + last observation time (row 3, NaN = None;
+ *                     controllers/__init__.py:229-230, 262-271); LQR-only callers may pass NULL,
+ *                     LQI-only callers a [3][n] array
  *   time   t[n]       per-episode accumulated time (t += dt, quadcopter_env.py:191)
  *   gains  K[kcols*4][m] SoA: element (row r, col c) of episode e at
  *                     K[(r*kcols + c)*m + e], with m = n (per-episode gains)
  *                     or m = 1 (one shared gain matrix, k_per_episode = 0).
+ *                     k_cols = 6: RiccatiLQRController / LQRController (4x6),
+ *                     9: LQI (4x9), 3: PIDController — K[9][m] = kp[3], ki[3], kd[3]
+ *                     (controllers/__init__.py:196-203).
  */
 #ifndef QUADTRACK_H
 #define QUADTRACK_H
@@ -141,7 +147,7 @@ typedef struct qt_batch {
   const double* plant_mass;     /* [n] or NULL -> env.mass */
   const double* hover_thrust;   /* [n] or NULL -> ctrl.hover_thrust */
   const double* K;              /* gains, layout above */
-  int32_t k_cols;               /* 6 (LQR) or 9 (LQI) */
+  int32_t k_cols;               /* 6 (LQR, heuristic LQR), 9 (LQI) or 3 (PID) */
   int32_t k_per_episode;        /* 0: one shared K (m = 1), 1: m = n */
   int32_t k_structured;         /* 1: the caller asserts every K entry outside the per-axis
                                    pattern (z->thrust, y->roll, x->pitch) is exactly 0, as the
@@ -153,7 +159,7 @@ typedef struct qt_batch {
 /* Mutable per-episode rollout state, all [.][n] SoA device arrays. */
 typedef struct qt_state {
   double* x;          /* [12][n] */
-  double* integ;      /* [3][n]  LQI integral (may be NULL when !use_lqi) */
+  double* integ;      /* [3][n] LQI integral | [4][n] PID integral + last time (NULL for LQR) */
   double* t;          /* [n] */
   double* acc;        /* [QT_ACC_ROWS][n] */
   double* target;     /* [9][n] target p,v,a at t (the observation the controller sees next) */
@@ -187,7 +193,9 @@ int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo
                     double* out, void* stream);
 
 /* The fused closed loop: `nsteps` iterations of
-   compute_action (riccati_lqr.py:779-967) -> env.step (quadcopter_env.py:152-232)
+   compute_action (riccati_lqr.py:779-967; k_cols 3: PIDController.compute_action,
+   controllers/__init__.py:243-379, with the observation time = the env time)
+   -> env.step (quadcopter_env.py:152-232)
    per episode, register-resident, with the Evaluator's per-episode metric
    accumulation fused (eval.py:119-159, utils/metrics.py:264-338).  Episodes that
    are done stay frozen.  May be called repeatedly (chunks).  If rec != NULL it
@@ -221,7 +229,12 @@ int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* a
    pos(3), target vel(3), target acc(3).  integ[3][n] is updated in LQI mode.
    action[4][n] out; saturated[n] (0/1) out (may be NULL); diag[16][n] (may be
    NULL) receives get_control_components() (969-978): state_error(6),
-   feedback_u(4), ff_velocity_term(3), ff_acceleration_term(3). */
+   feedback_u(4), ff_velocity_term(3), ff_acceleration_term(3).
+   k_cols = 6 with heuristic gains is LQRController.compute_action
+   (controllers/__init__.py:576-690).  k_cols = 3 is PIDController.compute_action
+   (controllers/__init__.py:243-379): obs[16][n] (row 15 = observation["time"]),
+   integ[4][n] (integral error, last time; NaN = None) updated, saturated = 0,
+   diag[18][n]: p, i, d, ff_velocity, ff_acceleration terms, total correction. */
 int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs,
                       double* integ, double* action, int8_t* saturated, double* diag, void* stream);
 

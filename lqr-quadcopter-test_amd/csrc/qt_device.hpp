@@ -470,9 +470,12 @@ __device__ __forceinline__ int termination_fast(const qt_env_params& e, double t
 // diagonal Q/R, riccati_lqr.py:602-700).  With finite errors (a running
 // episode) adding those exact zeros changes nothing, so both forms agree bit
 // for bit.
+//
+// KC == 3 is the PID controller: k = kp[3], ki[3], kd[3] (PIDController,
+// controllers/__init__.py:196-203); KS only marks that it never commands yaw.
 template <int KC, bool KS>
 struct Gains {
-  static constexpr int kCount = KS ? (KC == 9 ? 9 : 6) : 4 * KC;
+  static constexpr int kCount = KC == 3 ? 9 : (KS ? (KC == 9 ? 9 : 6) : 4 * KC);
   double k[kCount];
 };
 
@@ -590,6 +593,89 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
     for (int i = 0; i < 3; ++i) diag[10 + i] = ffv[i], diag[13 + i] = ffa[i];
   }
   return (u[0] != raw0) || (u[1] != raw1) || (u[2] != raw2) || (u[3] != raw3);
+}
+
+// PIDController.compute_action (controllers/__init__.py:243-379) given the
+// observation (quad p, v; target p, v, a) and its time `now`.  integ[4]:
+// integral error xyz and the last observation time (NaN = None, 263-265).
+// The integral advances by pos_error * dt only when dt > 0 and is clipped to
+// +-integral_limit (266-271); yaw rate is always 0 (373).  diag (optional, 18):
+// p, i, d, ff_velocity, ff_acceleration terms and the total correction
+// (get_control_components, 346-353).
+// FAST: gains, hover thrust, state and integral are known finite.
+template <bool FF, bool FAST = false>
+__device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, const double* g, double hover,
+                                                   const double* qp, const double* qv, const Target& tg, double now,
+                                                   double* integ, double* u, double* diag = nullptr) {
+  const double *kp = g, *ki = g + 3, *kd = g + 6;
+  double ep[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ep[i] = tg.p[i] - qp[i];
+  const double last = integ[3];
+  const double dt = last != last ? 0.0 : now - last;
+  integ[3] = now;
+  const double lim = c.integral_limit;
+  if (FAST) {  // select, not branch: the update is a handful of FMAs
+    const bool upd = dt > 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double v = clipd(integ[i] + ep[i] * dt, -lim, lim);
+      integ[i] = upd ? v : integ[i];
+    }
+  } else if (dt > 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i] + ep[i] * dt, -lim, lim);
+  }
+  if (FF && c.feedforward_enabled) {
+    const double vm = norm3(tv[0], tv[1], tv[2]);
+    if (vm > c.ff_max_velocity && vm > 0) {
+      const double scl = c.ff_max_velocity / vm;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) tv[i] = tv[i] * scl;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      tv[i] = (1.0 + c.ff_velocity_gain[i]) * tv[i];
+      ffv[i] = kd[i] * c.ff_velocity_gain[i] * tv[i] / (1.0 + c.ff_velocity_gain[i]);
+    }
+    double ac[3] = {tg.a[0], tg.a[1], tg.a[2]};
+    const double am = norm3(ac[0], ac[1], ac[2]);
+    if (am > c.ff_max_acceleration && am > 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ac[i] = ac[i] / am * c.ff_max_acceleration;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ffa[i] = c.ff_acceleration_gain[i] * ac[i];
+  }
+  double p[3], it[3], d[3], corr[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    p[i] = kp[i] * ep[i];
+    it[i] = ki[i] * integ[i];
+    d[i] = kd[i] * (tv[i] - qv[i]);
+    corr[i] = ((p[i] + it[i]) + d[i]) + ffa[i];
+  }
+  const double raw0 = hover + corr[2], raw1 = -corr[1], raw2 = corr[0];
+  u[0] = clip_num(raw0, c.min_thrust, c.max_thrust);
+  u[1] = clip_num(raw1, -c.max_rate, c.max_rate);
+  u[2] = clip_num(raw2, -c.max_rate, c.max_rate);
+  u[3] = 0.0;
+  if (!FAST && !isfinite((raw0 + raw1) + raw2)) {  // np.clip keeps NaN
+    u[0] = raw0 != raw0 ? raw0 : u[0];
+    u[1] = raw1 != raw1 ? raw1 : u[1];
+    u[2] = raw2 != raw2 ? raw2 : u[2];
+  }
+  if (diag) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      diag[i] = p[i];
+      diag[3 + i] = it[i];
+      diag[6 + i] = d[i];
+      diag[9 + i] = ffv[i];
+      diag[12 + i] = ffa[i];
+      diag[15 + i] = corr[i];
+    }
+  }
 }
 
 }  // namespace qt

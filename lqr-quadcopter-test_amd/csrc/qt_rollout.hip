@@ -75,6 +75,7 @@ struct BatchDev {
   const double* plant_mass;
   const double* hover;
   const double* K;
+  int32_t k_cols;
   int32_t k_per_episode;
   const int32_t* order;
   int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
@@ -105,7 +106,7 @@ __device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<
   const int64_t col = b.k_per_episode ? ep : 0;  // shared: uniform address -> scalar loads
 #pragma unroll
   for (int j = 0; j < Gains<KC, KS>::kCount; ++j) {
-    const int idx = KS ? structured_index<KC>(j) : j;
+    const int idx = (KS && KC != 3) ? structured_index<KC>(j) : j;
     G.k[j] = b.K[(int64_t)idx * m + col];
   }
 }
@@ -144,9 +145,10 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev
   for (int i = 0; i < 3; ++i) st.x[i * n + ep] = tg.p[i] + off[i * n + ep];
 #pragma unroll
   for (int i = 3; i < 12; ++i) st.x[i * n + ep] = 0.0;
-  if (st.integ) {
+  if (st.integ) {  // fresh controller (riccati_lqr.py:1073-1086, controllers/__init__.py:389-393)
 #pragma unroll
     for (int i = 0; i < 3; ++i) st.integ[i * n + ep] = 0.0;
+    if (b.k_cols == 3) st.integ[3 * n + ep] = NAN;  // PID: no previous observation time
   }
   st.t[ep] = 0.0;
 #pragma unroll
@@ -181,7 +183,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     if (QT_ABLATE & QT_ABL_CONTROLLER) {
       u[0] = hover, u[1] = u[2] = u[3] = 0.0;
     } else {
-      compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u);
+      if constexpr (KC == 3)
+        compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
+      else
+        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u);
     }
     // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
     if (!(QT_ABLATE & QT_ABL_METRICS)) {
@@ -266,13 +271,13 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   Gains<KC, KS> G;
   load_gains<KC, KS>(b, ep, G);
 
-  double x[12], integ[3] = {0, 0, 0};
+  // integ: LQI integral (KC 9) | PID integral error + last observation time (KC 3)
+  constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
+  double x[12], integ[4] = {0, 0, 0, NAN};
 #pragma unroll
   for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
-  if (KC == 9) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) integ[i] = st.integ[i * n + ep];
-  }
+  for (int i = 0; i < NI; ++i) integ[i] = st.integ[i * n + ep];
   Target tg;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -308,10 +313,8 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
 
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
-  if (KC == 9) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) st.integ[i * n + ep] = integ[i];
-  }
+  for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     st.target[i * n + ep] = tg.p[i];
@@ -380,7 +383,9 @@ __global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchD
   const int64_t n = b.n, ep = episode_of(b, slot);
   Gains<KC, false> G;
   load_gains<KC, false>(b, ep, G);
-  double qp[3], qv[3], in[3] = {0, 0, 0}, u[4];
+  constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
+  constexpr int ND = KC == 3 ? 18 : 16;
+  double qp[3], qv[3], in[4] = {0, 0, 0, NAN}, u[4];
   Target tg;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -390,23 +395,23 @@ __global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchD
     tg.v[i] = obs[(9 + i) * n + ep];
     tg.a[i] = obs[(12 + i) * n + ep];
   }
-  if (KC == 9) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) in[i] = integ[i * n + ep];
-  }
+  for (int i = 0; i < NI; ++i) in[i] = integ[i * n + ep];
   const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
-  double dg[16];
-  const bool sat = compute_action<KC, true, false>(c, G, hover, qp, qv, tg, in, u, dg);
+  double dg[ND];
+  bool sat = false;
+  if constexpr (KC == 3)
+    compute_action_pid<true>(c, G.k, hover, qp, qv, tg, obs[15 * n + ep], in, u, dg);  // row 15: time
+  else
+    sat = compute_action<KC, true, false>(c, G, hover, qp, qv, tg, in, u, dg);
 #pragma unroll
   for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
   if (diag) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) diag[i * n + ep] = dg[i];
+    for (int i = 0; i < ND; ++i) diag[i * n + ep] = dg[i];
   }
-  if (KC == 9) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) integ[i * n + ep] = in[i];
-  }
+  for (int i = 0; i < NI; ++i) integ[i * n + ep] = in[i];
   if (sat_out) sat_out[ep] = sat;
 }
 
@@ -645,8 +650,8 @@ __global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, co
 }
 
 BatchDev to_dev(const qt_batch* b) {
-  return BatchDev{b->n, b->motion, b->pattern, b->plant_mass, b->hover_thrust, b->K, b->k_per_episode, b->order,
-                  0, b->n};
+  return BatchDev{b->n,     b->motion,        b->pattern, b->plant_mass, b->hover_thrust, b->K,
+                  b->k_cols, b->k_per_episode, b->order,   0,             b->n};
 }
 
 int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
@@ -695,7 +700,12 @@ void launch_rollout(bool ff, bool ks, int motion, int grid, hipStream_t s, const
                     const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                     double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
-  if (ff) {
+  if constexpr (KC == 3) {  // PID never commands yaw (controllers/__init__.py:373): the yaw-at-rest flavour applies
+    if (ff)
+      launch_rollout_motion<3, true, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+    else
+      launch_rollout_motion<3, false, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+  } else if (ff) {
     if (ks)
       launch_rollout_motion<KC, true, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
     else
@@ -728,8 +738,8 @@ int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offs
 int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit, const qt_batch* batch,
                qt_state st, int32_t nsteps, double* rec, void* stream) {
   if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
-  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
-  if (!valid_state(st, batch->k_cols == 9)) return QT_EINVAL;
+  if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (!valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
   if (batch->n == 0 || nsteps == 0) return QT_OK;
   const BatchDev b = to_dev(batch);
   const int grid = grid_of(batch->n);
@@ -739,6 +749,8 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   const bool ks = batch->k_structured != 0;
   if (batch->k_cols == 9)
     launch_rollout<9>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+  else if (batch->k_cols == 3)
+    launch_rollout<3>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   else
     launch_rollout<6>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   return check_launch();
@@ -748,8 +760,8 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream) {
   if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
-  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
-  if (!valid_state(st, batch->k_cols == 9)) return QT_EINVAL;
+  if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (!valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
   if (nseg < 0 || (nseg > 0 && (!seg_motion || !seg_end))) return QT_EINVAL;
   int64_t prev = 0;
   for (int32_t i = 0; i < nseg; ++i) {
@@ -769,6 +781,8 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
     const int grid = grid_of(b.slot_end - b.slot0);
     if (batch->k_cols == 9)
       launch_rollout<9>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    else if (batch->k_cols == 3)
+      launch_rollout<3>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
     else
       launch_rollout<6>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
@@ -788,12 +802,14 @@ int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* a
 int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs, double* integ,
                       double* action, int8_t* saturated, double* diag, void* stream) {
   if (!ctrl || !batch || !obs || !action || !batch->K || batch->n < 0) return QT_EINVAL;
-  if (batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
-  if (batch->k_cols == 9 && !integ) return QT_EINVAL;
+  if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (batch->k_cols != 6 && !integ) return QT_EINVAL;
   if (batch->n == 0) return QT_OK;
   hipStream_t s = (hipStream_t)stream;
   if (batch->k_cols == 9)
     action_kernel<9><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
+  else if (batch->k_cols == 3)
+    action_kernel<3><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
   else
     action_kernel<6><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
   return check_launch();

@@ -10,7 +10,17 @@ a visible GPU the numeric calls raise.
 """
 
 from . import _abi
-from .controllers import BaseController, BatchedRiccatiLQR, LQRController, RiccatiLQRController, solve_dare
+from .controllers import (
+    BaseController,
+    BatchedLQR,
+    BatchedPID,
+    BatchedRiccatiLQR,
+    LQRController,
+    PIDController,
+    RiccatiLQRController,
+    batched_controller,
+    solve_dare,
+)
 from .env import BatchedQuadcopterEnv, EnvConfig, QuadcopterEnv, TargetMotion
 from .eval import Evaluator, evaluate_batched, load_controller
 from .rollout import RolloutResult, run_closed_loop
@@ -18,7 +28,8 @@ from .utils import EpisodeMetrics, EvaluationSummary, SuccessCriteria, compute_e
 
 __version__ = "0.1.0"
 
-__all__ = ["BaseController", "BatchedRiccatiLQR", "LQRController", "RiccatiLQRController", "solve_dare",
+__all__ = ["BaseController", "BatchedLQR", "BatchedPID", "BatchedRiccatiLQR", "LQRController", "PIDController",
+           "RiccatiLQRController", "batched_controller", "solve_dare",
            "BatchedQuadcopterEnv", "EnvConfig", "QuadcopterEnv", "TargetMotion", "Evaluator", "evaluate_batched",
            "load_controller", "RolloutResult", "run_closed_loop", "EpisodeMetrics", "EvaluationSummary",
            "SuccessCriteria", "compute_episode_metrics", "_abi"]

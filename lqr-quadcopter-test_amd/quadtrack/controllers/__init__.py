@@ -2,7 +2,8 @@
 the Riccati controller, its heuristic-LQR fallback and the plugin base)."""
 
 from .base import ACTION_KEYS, DEFAULT_ACTION_LIMITS, ActionLimits, BaseController, validate_action
-from .lqr import LQRController, heuristic_gains
+from .lqr import BatchedLQR, LQRController, heuristic_gains
+from .pid import BatchedPID, PIDController
 from .riccati_lqr import (
     BatchedRiccatiLQR,
     RiccatiLQRController,
@@ -11,10 +12,27 @@ from .riccati_lqr import (
     solve_dare,
 )
 
-VALID_CONTROLLER_TYPES = ("lqr", "riccati_lqr", "lqi")
+VALID_CONTROLLER_TYPES = ("lqr", "pid", "riccati_lqr", "lqi")
+
+
+def batched_controller(controller_type: str = "riccati_lqr", config: dict | None = None, device=None, **per_episode):
+    """Batched gains for the fused closed loop by controller type (the
+    batched counterpart of eval.load_controller, eval.py:472-513):
+    "riccati_lqr" / "lqi" -> BatchedRiccatiLQR, "lqr" -> BatchedLQR (heuristic
+    gains), "pid" -> BatchedPID.  Per-episode arrays go to the constructor."""
+    config = dict(config or {})
+    if controller_type == "lqi":
+        config["use_lqi"] = True
+        config.setdefault("q_int", [0.01, 0.01, 0.1])
+        controller_type = "riccati_lqr"
+    cls = {"riccati_lqr": BatchedRiccatiLQR, "lqr": BatchedLQR, "pid": BatchedPID}.get(controller_type)
+    if cls is None:
+        raise ValueError(f"Unknown controller type: {controller_type}")
+    return cls(config, device=device, **per_episode)
 
 __all__ = [
     "ACTION_KEYS", "DEFAULT_ACTION_LIMITS", "ActionLimits", "BaseController", "validate_action", "LQRController",
-    "heuristic_gains", "BatchedRiccatiLQR", "RiccatiLQRController", "build_augmented_lqi_system",
-    "build_linearized_system", "solve_dare", "VALID_CONTROLLER_TYPES",
+    "BatchedLQR", "PIDController", "BatchedPID", "batched_controller", "heuristic_gains", "BatchedRiccatiLQR",
+    "RiccatiLQRController", "build_augmented_lqi_system", "build_linearized_system", "solve_dare",
+    "VALID_CONTROLLER_TYPES",
 ]

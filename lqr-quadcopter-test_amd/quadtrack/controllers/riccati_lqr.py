@@ -197,24 +197,33 @@ def _validate_observation(observation: dict) -> None:
 
 class _OneEpisodeKernel:
     """Device buffers for running qt_compute_action on one observation.
-    One upload (obs) and one download (action | integral | diagnostics | flag)
-    per call."""
+    One upload (obs, plus the integral state when the host owns it) and one
+    download (action | integral | diagnostics | saturation flag) per call.
+    Integral / diagnostics: 3 / 16 values (LQR, LQI), 4 / 18 (PID: integral
+    error + last observation time; p, i, d, ff terms, total correction)."""
 
     def __init__(self, K: np.ndarray, k_cols: int, device):
         self.dev = _abi.require_gpu(device)
         self.k_cols = k_cols
+        self.ni, self.nd = (4, 18) if k_cols == 3 else (3, 16)
         self.K = torch.as_tensor(np.ascontiguousarray(K[:, :k_cols].reshape(-1, 1)), dtype=F64, device=self.dev)
-        self.buf = torch.zeros(24, dtype=F64, device=self.dev)  # action 4 | integ 3 | diag 16 | flag
+        self.buf = torch.zeros(4 + self.ni + self.nd + 1, dtype=F64, device=self.dev)
 
     def zero_integral(self):
         self.buf[4:7].zero_()
 
-    def __call__(self, ctrl: CtrlParams, obs15: np.ndarray):
-        obs = torch.as_tensor(obs15.reshape(15, 1), dtype=F64).to(self.dev)
+    def __call__(self, ctrl: CtrlParams, obs: np.ndarray, integ: np.ndarray | None = None):
+        no = obs.size
+        host = obs if integ is None else np.concatenate([obs, integ])
+        up = torch.as_tensor(np.ascontiguousarray(host, dtype=np.float64).reshape(-1, 1)).to(self.dev)
         b = self.buf
-        act, sat = core.compute_action(ctrl, self.K, self.k_cols, obs, b[4:7].view(3, 1), None, b[7:23].view(16, 1))
+        i0, d0 = 4, 4 + self.ni
+        if integ is not None:
+            b[i0:d0].copy_(up[no:, 0])
+        act, sat = core.compute_action(ctrl, self.K, self.k_cols, up[:no], b[i0:d0].view(self.ni, 1), None,
+                                       b[d0:d0 + self.nd].view(self.nd, 1))
         b[0:4].copy_(act.view(4))
-        b[23] = sat.to(F64)[0]
+        b[-1] = sat.to(F64)[0]
         return b.cpu().numpy()
 
 
@@ -411,6 +420,8 @@ class BatchedRiccatiLQR:
     configs 4-5).  Failed problems fall back to the heuristic gains per
     episode (riccati_lqr.py:737-777) unless fallback_on_failure is False.
     """
+
+    kind = "riccati_lqr"
 
     def __init__(self, config: dict | None = None, device=None, *, q_pos=None, q_vel=None, r_controls=None,
                  q_int=None, mass=None, Q=None, R=None):

@@ -33,8 +33,8 @@ class EpisodeBatch:
     device: torch.device
     pattern: torch.Tensor                     # [4, n] raw draws
     offset: torch.Tensor                      # [3, n]
-    K: torch.Tensor                           # [4*k_cols, n] or [4*k_cols, 1]
-    k_cols: int
+    K: torch.Tensor                           # [4*k_cols, n] or [4*k_cols, 1] ([9, .] for PID)
+    k_cols: int                               # 6 LQR | 9 LQI | 3 PID (gains kp, ki, kd)
     motion: torch.Tensor | None = None        # [n] int8
     plant_mass: torch.Tensor | None = None    # [n]
     hover: torch.Tensor | None = None         # [n]
@@ -62,7 +62,7 @@ class RolloutState:
     """Mutable per-episode state (qt_state)."""
 
     x: torch.Tensor       # [12, n]
-    integ: torch.Tensor   # [3, n]
+    integ: torch.Tensor   # [4, n]: LQI integral (rows 0-2) | PID integral error + last observation time
     t: torch.Tensor       # [n]
     acc: torch.Tensor     # [ACC_ROWS, n]
     target: torch.Tensor  # [9, n]
@@ -70,12 +70,20 @@ class RolloutState:
     @classmethod
     def empty(cls, n: int, device) -> "RolloutState":
         z = lambda *s: torch.zeros(*s, dtype=F64, device=device)  # noqa: E731
-        return cls(z(12, n), z(3, n), z(n), z(ACC_ROWS, n), z(9, n))
+        return cls(z(12, n), z(INTEG_ROWS, n), z(n), z(ACC_ROWS, n), z(9, n))
 
     def c_state(self) -> State:
         s = State()
         s.x, s.integ, s.t, s.acc, s.target = (ptr(v) for v in (self.x, self.integ, self.t, self.acc, self.target))
         return s
+
+
+INTEG_ROWS = 4
+
+
+def gain_rows(k_cols: int) -> int:
+    """Rows of the SoA gain array: 4 x k_cols, or kp/ki/kd (9) for PID."""
+    return 9 if k_cols == 3 else 4 * k_cols
 
 
 _AXIS_PATTERN = {6: [(0, 2), (0, 5), (1, 1), (1, 4), (2, 0), (2, 3)]}
@@ -84,7 +92,10 @@ _AXIS_PATTERN[9] = _AXIS_PATTERN[6] + [(0, 8), (1, 7), (2, 6)]
 
 def gains_structured(K: torch.Tensor, k_cols: int) -> bool:
     """True when every entry of K ([4*k_cols, m]) outside the per-axis pattern
-    is exactly zero (qt_batch.k_structured)."""
+    is exactly zero (qt_batch.k_structured).  PID gains (k_cols 3) are
+    per-axis by construction."""
+    if k_cols == 3:
+        return True
     mask = torch.ones(4 * k_cols, dtype=torch.bool, device=K.device)
     for r, c in _AXIS_PATTERN[k_cols]:
         mask[r * k_cols + c] = False
@@ -107,10 +118,11 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
     n = batch.n
     _check_cols("pattern", batch.pattern, 4, n)
     _check_cols("offset", batch.offset, 3, n)
-    if batch.k_cols not in (6, 9):
-        raise ValueError("k_cols must be 6 or 9")
-    if batch.K.dim() != 2 or batch.K.shape[0] != 4 * batch.k_cols or batch.K.shape[1] not in (1, n):
-        raise ValueError(f"K must be [{4 * batch.k_cols}, 1 or {n}], got {tuple(batch.K.shape)}")
+    if batch.k_cols not in (3, 6, 9):
+        raise ValueError("k_cols must be 3 (PID), 6 (LQR) or 9 (LQI)")
+    rows = gain_rows(batch.k_cols)
+    if batch.K.dim() != 2 or batch.K.shape[0] != rows or batch.K.shape[1] not in (1, n):
+        raise ValueError(f"K must be [{rows}, 1 or {n}], got {tuple(batch.K.shape)}")
     for name in ("motion", "plant_mass", "hover", "order"):
         t = getattr(batch, name)
         if t is not None and (t.numel() != n or not t.is_contiguous()):
@@ -123,7 +135,7 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
             raise ValueError("order entries out of range")
     if st is not None:
         _check_cols("x", st.x, 12, n)
-        _check_cols("integ", st.integ, 3, n)
+        _check_cols("integ", st.integ, INTEG_ROWS, n)
         _check_cols("acc", st.acc, ACC_ROWS, n)
         _check_cols("target", st.target, 9, n)
         if st.t.numel() != n:
@@ -300,10 +312,17 @@ def env_step(env: EnvParams, batch: EpisodeBatch, action: torch.Tensor, st: Roll
 def compute_action(ctrl: CtrlParams, K: torch.Tensor, k_cols: int, obs: torch.Tensor, integ: torch.Tensor,
                    hover: torch.Tensor | None = None, diag: torch.Tensor | None = None):
     """obs [15, n] -> (action [4, n], saturated [n] bool); integ [3, n] updated in place (LQI);
-    diag [16, n] (optional) receives the control components."""
+    diag [16, n] (optional) receives the control components.  PID (k_cols 3): obs [16, n] with the
+    observation time in row 15, integ [4, n] (integral error, last time), diag [18, n]."""
     lib = _abi.load()
     n, dev = obs.shape[1], obs.device
-    _check_cols("obs", obs, 15, n)
+    _check_cols("obs", obs, 16 if k_cols == 3 else 15, n)
+    if K.dim() != 2 or K.shape[0] != gain_rows(k_cols) or K.shape[1] not in (1, n):
+        raise ValueError(f"K must be [{gain_rows(k_cols)}, 1 or {n}], got {tuple(K.shape)}")
+    if k_cols != 6 and (integ is None or integ.shape[0] < (4 if k_cols == 3 else 3) or integ.shape[-1] != n):
+        raise ValueError("integ must be [3, n] (LQI) or [4, n] (PID)")
+    if diag is not None:
+        _check_cols("diag", diag, 18 if k_cols == 3 else 16, n)
     b = Batch()
     b.n = n
     b.K = ptr(K)

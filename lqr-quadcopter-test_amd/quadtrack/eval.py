@@ -23,7 +23,13 @@ from typing import Callable
 
 import numpy as np
 
-from .controllers import BaseController, BatchedRiccatiLQR, LQRController, RiccatiLQRController
+from .controllers import (
+    BaseController,
+    LQRController,
+    PIDController,
+    RiccatiLQRController,
+    batched_controller,
+)
 from .env import EnvConfig, QuadcopterEnv
 from .env.config import as_env_config
 from .rollout import run_closed_loop
@@ -122,6 +128,8 @@ def load_controller(controller_type: str, checkpoint_path=None, config: dict | N
     config = config or {}
     if controller_type == "lqr":
         return LQRController(config=config)
+    if controller_type == "pid":
+        return PIDController(config=config)
     if controller_type == "riccati_lqr":
         return RiccatiLQRController(config=config)
     if controller_type == "lqi":
@@ -129,7 +137,7 @@ def load_controller(controller_type: str, checkpoint_path=None, config: dict | N
         cfg["use_lqi"] = True
         cfg.setdefault("q_int", [0.01, 0.01, 0.1])
         return RiccatiLQRController(config=cfg)
-    if controller_type in ("deep", "pid"):
+    if controller_type == "deep":
         raise NotImplementedError(f"controller type '{controller_type}' is outside the MI355X hot path")
     raise ValueError(f"Unknown controller type: {controller_type}")
 
@@ -140,12 +148,15 @@ def evaluate_batched(controller, env_config=None, num_episodes: int = 10, base_s
                      group=None, global_offset: int = 0) -> EvaluationSummary:
     """All episodes in one fused closed-loop launch (fresh controller each).
 
-    `controller` is a RiccatiLQRController (shared gains), a
-    BatchedRiccatiLQR (shared or per-episode gains) or a config dict."""
+    `controller` is a drop-in controller (RiccatiLQRController, LQRController,
+    PIDController: shared gains), a batched one (BatchedRiccatiLQR,
+    BatchedLQR, BatchedPID: shared or per-episode gains) or a config dict
+    (its "controller" key picks the type, default riccati_lqr)."""
     cfg = as_env_config(env_config)
     if isinstance(controller, dict):
-        controller = BatchedRiccatiLQR(controller)
-    elif isinstance(controller, RiccatiLQRController):
+        c = dict(controller)
+        controller = batched_controller(c.pop("controller", "riccati_lqr"), c)
+    elif isinstance(controller, (RiccatiLQRController, LQRController, PIDController)):
         controller = controller.to_batched()
     seeds = base_seed + global_offset + np.arange(num_episodes)
     res = run_closed_loop(controller, cfg, n=num_episodes, seeds=seeds, motion=motion, plant_mass=plant_mass,

@@ -23,7 +23,7 @@ import torch
 
 from . import _abi, core
 from ._abi import MET, MET_FIELDS, TERM_REASONS
-from .controllers.riccati_lqr import BatchedRiccatiLQR
+from .controllers.riccati_lqr import BatchedRiccatiLQR  # or BatchedLQR / BatchedPID: same batch interface
 from .env import seeding
 from .env.batched import motion_indices
 from .env.config import as_env_config

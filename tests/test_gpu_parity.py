@@ -46,8 +46,10 @@ def _cfg_list(s, key, n):
 
 @pytest.mark.parametrize("s", SCEN["scenarios"], ids=[s["name"] for s in SCEN["scenarios"]])
 def test_fused_rollout_matches_reference(qt, s):
-    """Per-scenario batch through qt_reset + qt_rollout + qt_episode_metrics."""
-    from quadtrack.controllers import BatchedRiccatiLQR
+    """Per-scenario batch through qt_reset + qt_rollout + qt_episode_metrics.
+    The scenario's "controller" key picks Riccati-LQR/LQI (default), the
+    heuristic LQRController ("lqr") or the PIDController ("pid")."""
+    from quadtrack.controllers import BatchedRiccatiLQR, batched_controller
     from quadtrack.rollout import run_closed_loop
 
     n = len(s["seeds"])
@@ -63,7 +65,8 @@ def test_fused_rollout_matches_reference(qt, s):
     plant_mass = None if uniform_env else [e.get("quadcopter", {}).get("mass", 1.0) for e in envs]
     env_cfg = envs[0] if uniform_env else base_env
     if all(json.dumps(c, sort_keys=True) == json.dumps(ctls[0], sort_keys=True) for c in ctls):
-        ctl = BatchedRiccatiLQR(ctls[0])
+        c0 = dict(ctls[0])
+        ctl = batched_controller(c0.pop("controller", "riccati_lqr"), c0)
     else:
         keys = {k for c in ctls for k in c}
         per = {k: [c[k] for c in ctls] for k in ("q_pos", "q_vel", "r_controls", "mass") if k in keys}
@@ -77,8 +80,8 @@ def test_fused_rollout_matches_reference(qt, s):
         np.testing.assert_allclose(met[i], ref[:, i], rtol=rtol, atol=tol, err_msg=f)
     fin = CL[s["name"] + "_final"]
     np.testing.assert_allclose(res.state.x.cpu().numpy().T, fin[:, :12], rtol=1e-8, atol=tol)
-    if ctl.use_lqi:
-        np.testing.assert_allclose(res.state.integ.cpu().numpy().T, fin[:, 12:], rtol=1e-8, atol=tol)
+    if ctl.use_lqi or ctl.kind == "pid":  # LQI integral state | PID integral error
+        np.testing.assert_allclose(res.state.integ[:3].cpu().numpy().T, fin[:, 12:], rtol=1e-8, atol=tol)
     if s["record"]:
         rec = res.record.cpu().numpy()  # [steps, 16, n]
         steps = CL["rec_steps"]
@@ -156,19 +159,21 @@ def test_chunked_equals_single_launch(qt):
     assert torch.equal(a.state.x, b.state.x)
 
 
-@pytest.mark.parametrize("case", ["linear_lqr", "sinusoidal_lqi", "figure8_ff", "mixed_mass", "circular_tight"])
+@pytest.mark.parametrize("case", ["linear_lqr", "sinusoidal_lqi", "figure8_ff", "mixed_mass", "circular_tight",
+                                  "pid_integral", "pid_ff_circular", "lqr_heuristic_ff"])
 def test_fast_path_equals_exact_path(qt, case):
     """The branch-light fast step (taken when the wave qualifies and nothing is
     recorded) against the exact step (forced by recording): the same decisions
     (counts, codes, steps) and the same values up to rounding (the two code
     paths are contracted into FMAs differently by the compiler)."""
-    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.controllers import BatchedRiccatiLQR, batched_controller
     from quadtrack.rollout import run_closed_loop
 
     n = 1024
     env = {}
     kw = {}
     ctl_cfg = {"dt": 0.01}
+    kind = "riccati_lqr"
     if case == "linear_lqr":
         env = {"target": {"motion_type": "linear"}}
     elif case == "sinusoidal_lqi":
@@ -179,10 +184,21 @@ def test_fast_path_equals_exact_path(qt, case):
         ctl_cfg.update(feedforward_enabled=True, ff_velocity_gain=[0.1, 0.1, 0.1], ff_acceleration_gain=[0.05] * 3)
     elif case == "mixed_mass":
         kw = dict(motion=[i % 5 for i in range(n)], plant_mass=0.8 + 0.4 * np.arange(n) / n)
-    else:  # fast yaw/tilt motion: large gains drive the attitude to the clamps
+    elif case == "circular_tight":  # fast yaw/tilt motion: large gains drive the attitude to the clamps
         env = {"target": {"motion_type": "circular", "speed": 4.0, "radius": 1.0}}
         ctl_cfg.update(q_pos=[10.0, 10.0, 40.0], r_controls=[0.05, 0.05, 0.05, 0.05])
-    ctl = BatchedRiccatiLQR(ctl_cfg)
+    elif case == "pid_integral":
+        kind, env = "pid", {"target": {"motion_type": "sinusoidal"}}
+        ctl_cfg = {"kp_pos": [0.02, 0.02, 5.0], "ki_pos": [0.005, 0.005, 0.8], "integral_limit": 1.5}
+    elif case == "pid_ff_circular":
+        kind, env = "pid", {"target": {"motion_type": "circular", "speed": 3.0}}
+        ctl_cfg = {"feedforward_enabled": True, "ff_velocity_gain": [0.3, 0.3, 0.1], "ff_acceleration_gain": 0.2,
+                   "ki_pos": 0.01, "integral_limit": 0.5, "ff_max_velocity": 2.5}
+    else:
+        kind, env = "lqr", {"target": {"motion_type": "figure8"}}
+        ctl_cfg = {"q_pos": [2e-4, 3e-4, 20.0], "feedforward_enabled": True, "ff_velocity_gain": 0.2,
+                   "ff_acceleration_gain": [0.1, 0.1, 0.3]}
+    ctl = BatchedRiccatiLQR(ctl_cfg) if kind == "riccati_lqr" else batched_controller(kind, ctl_cfg)
     fast = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), **kw)
     exact = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), record=True, **kw)
     mf, me = fast.metrics.cpu().numpy(), exact.metrics.cpu().numpy()
@@ -358,6 +374,66 @@ def test_controller_kernel_sequences(qt):
                                            atol=1e-14)
 
 
+def test_pid_and_heuristic_lqr_drop_in_sequences(qt):
+    """PIDController / LQRController drop-ins (GPU controller kernel, k_cols 3 /
+    6) over the reference's observation sequence with observation times
+    (repeated and decreasing ones: the PID integral only advances on dt > 0)."""
+    from quadtrack.eval import load_controller
+
+    A = np.load(os.path.join(GOLDEN, "controller_actions.npz"))
+    cases = json.loads(str(A["cases_json"]))
+    for ci, cfg in enumerate(cases):
+        cfg = dict(cfg)
+        kind = cfg.pop("controller")
+        ctl = load_controller(kind, config=cfg)
+        if kind == "lqr":
+            np.testing.assert_allclose(ctl.K, A[f"case{ci}_K"], rtol=1e-15)
+        for k, o in enumerate(A["obs"]):
+            obs = {"quadcopter": {"position": o[0:3], "velocity": o[3:6], "attitude": np.zeros(3),
+                                  "angular_velocity": np.zeros(3)},
+                   "target": {"position": o[6:9], "velocity": o[9:12], "acceleration": o[12:15]},
+                   "time": float(A["time"][k])}
+            a = ctl.compute_action(obs)
+            got = [a["thrust"], a["roll_rate"], a["pitch_rate"], a["yaw_rate"]]
+            np.testing.assert_allclose(got, A[f"case{ci}_action"][k], rtol=1e-12, atol=1e-12, err_msg=f"{ci} {k}")
+            if kind == "pid":
+                np.testing.assert_allclose(ctl.integral_error, A[f"case{ci}_integral"][k], rtol=1e-13, atol=1e-15)
+                comp = ctl.get_control_components()
+                np.testing.assert_allclose(comp["p_term"] + comp["i_term"] + comp["d_term"]
+                                           + comp["ff_acceleration_term"], comp["total_correction"], rtol=1e-12,
+                                           atol=1e-12)
+        ctl.reset()
+        if kind == "pid":
+            assert ctl._last_time is None and not ctl.integral_error.any()
+
+
+@pytest.mark.parametrize("kind", ["pid", "lqr"])
+def test_pid_and_heuristic_lqr_batch_vs_oracle(qt, kind):
+    """4,096 full episodes (linear target, per-episode mass) of the PID /
+    heuristic-LQR closed loop on the fast kernel against the oracle."""
+    from quadtrack.controllers import batched_controller
+    from quadtrack.rollout import run_closed_loop
+
+    n = 4096
+    mass = 0.8 + 0.4 * np.random.default_rng(5).random(n)
+    cfg = {"ki_pos": [0.01, 0.01, 0.3], "integral_limit": 2.0} if kind == "pid" else {"r_rate": 0.5}
+    ctl = batched_controller(kind, cfg, mass=mass)
+    env_cfg = {"target": {"motion_type": "linear"}}
+    res = run_closed_loop(ctl, env_cfg, n=n, seeds=np.arange(n), plant_mass=mass)
+    env = O.env_params(env_cfg)
+    c, K, kc, _, _ = O.controller({"controller": kind, **cfg})
+    pat, off = O.draws("linear", range(n))
+    x0 = np.array([O.initial_state(env, env.motion, pat[i], off[i]) for i in range(n)])
+    Kd = np.broadcast_to(np.asarray(K, float).reshape(1, -1), (n, K.size)).copy()
+    hover = mass * 9.81
+    ref, xf, integ, _ = O.rollout(env, c, O.criteria(), None, pat, mass, hover, Kd, kc, True, x0)
+    met = res.metrics.cpu().numpy().T
+    np.testing.assert_allclose(met, ref, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(res.state.x.cpu().numpy().T, xf, rtol=1e-8, atol=TOL)
+    if kind == "pid":
+        np.testing.assert_allclose(res.state.integ[:3].cpu().numpy().T, integ, rtol=1e-8, atol=TOL)
+
+
 def test_lqi_known_answers(qt):
     """test_env_dynamics.py:3745-3851 known answers through the GPU controller."""
     from quadtrack import RiccatiLQRController
@@ -503,3 +579,22 @@ def test_evaluate_batched_vs_evaluator(qt):
     for k in ("mean_on_target_ratio", "mean_tracking_error", "std_tracking_error", "mean_control_effort"):
         assert getattr(bat, k) == pytest.approx(getattr(seq, k), rel=1e-9, abs=1e-12), k
     assert bat.best_episode_idx == seq.best_episode_idx
+
+
+@pytest.mark.parametrize("kind", ["pid", "lqr"])
+def test_evaluate_batched_vs_evaluator_pid_lqr(qt, kind):
+    """Same for the PID (default gains: integral clipped to 0, so nothing
+    carries over) and heuristic-LQR drop-ins."""
+    from quadtrack import Evaluator, evaluate_batched, load_controller
+    from quadtrack.env import EnvConfig
+
+    cfg = EnvConfig.from_dict({"target": {"motion_type": "sinusoidal"}, "simulation": {"max_episode_time": 2.0},
+                               "logging": {"enabled": False}})
+    ctl = load_controller(kind)
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        seq = Evaluator(ctl, cfg, output_dir=d).evaluate(num_episodes=3, base_seed=7, verbose=False)
+    bat = evaluate_batched(ctl, cfg, num_episodes=3, base_seed=7)
+    for k in ("mean_on_target_ratio", "mean_tracking_error", "std_tracking_error", "mean_control_effort"):
+        assert getattr(bat, k) == pytest.approx(getattr(seq, k), rel=1e-9, abs=1e-12), k
