@@ -570,14 +570,19 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
       uf[r] = a;
     }
   }
-  const double raw0 = hover + uf[0] + ffa[2];
-  const double raw1 = uf[1] + -ffa[1];
-  const double raw2 = uf[2] + ffa[0];
+  // Without feed-forward the reference adds ff terms that are exactly 0.0;
+  // x + 0.0 differs from x only for x = -0.0, which no later operation
+  // distinguishes (clips, products and sums all treat the zeros alike).
+  const double raw0 = FF ? hover + uf[0] + ffa[2] : hover + uf[0];
+  const double raw1 = FF ? uf[1] + -ffa[1] : uf[1];
+  const double raw2 = FF ? uf[2] + ffa[0] : uf[2];
   const double raw3 = uf[3];
   u[0] = clip_num(raw0, c.min_thrust, c.max_thrust);
   u[1] = clip_num(raw1, -c.max_rate, c.max_rate);
   u[2] = clip_num(raw2, -c.max_rate, c.max_rate);
-  u[3] = clip_num(raw3, -c.max_rate, c.max_rate);
+  // structured gains have no yaw row: clip(0, -max_rate, max_rate) = 0 for
+  // the max_rate >= 0 that fast_path_ok requires
+  u[3] = (KS && FAST) ? 0.0 : clip_num(raw3, -c.max_rate, c.max_rate);
   if (!FAST && !isfinite((raw0 + raw1) + (raw2 + raw3))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
     u[0] = raw0 != raw0 ? raw0 : u[0];
     u[1] = raw1 != raw1 ? raw1 : u[1];

@@ -83,6 +83,27 @@ QT_HD void small_sincos(double d, double* s, double* c) {
   *c = fma(z, q, 1.0);
 }
 
+#if defined(__HIPCC__)
+// sqrt(x) for the metric accumulators of the fast step: the device library's
+// correctly rounded sequence (v_rsq_f64 + two Goldschmidt / Newton
+// corrections) without its rescaling of x < 2^-767.  Bit-identical to sqrt
+// for x >= 2^-767 and for x == 0; below that (a tracking error under 1e-115 m
+// or a command norm under 1e-115) it may differ in the last bits, which no
+// metric can show.  x must be finite and >= 0.
+__device__ __forceinline__ double sqrt_noscale(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return x == 0.0 ? x : g;
+}
+#endif
+
 // numpy's float remainder: (a % b) with the sign of b, b = 2*pi here
 // (quadcopter_env.py:457).  For |a| < 4*pi the single subtraction / addition
 // is exact (Sterbenz), so it equals fmod bit for bit; larger |a| use fmod.

@@ -176,6 +176,13 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
+  // squared pre-step tracking error: the previous step's post-step error
+  // (same positions, same target: positions are not constrained), carried
+  double se_pre;
+  {
+    const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+    se_pre = ep0 * ep0 + ep1 * ep1 + ep2 * ep2;
+  }
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -190,14 +197,21 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     }
     // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
     if (!(QT_ABLATE & QT_ABL_METRICS)) {
-      const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-      const double err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+      double err, un;
+      if (FAST) {
+        err = sqrt_noscale(se_pre);
+        un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      } else {
+        const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+        err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+        un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      }
       a.sum_e += err;
       a.sum_e2 += err * err;
       if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
       const bool on = err <= R;
       a.on_pre += on;
-      a.sum_u += sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      a.sum_u += un;
       overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
       a.prev_on = on;
     }
@@ -209,6 +223,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
+      se_pre = se;
       const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
       if (ok) {
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
