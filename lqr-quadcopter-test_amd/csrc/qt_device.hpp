@@ -179,10 +179,19 @@ struct Trig {
 // structured gain never commands yaw, u[3] = 0, so a yaw that starts at zero
 // stays zero: quadcopter_env.py:412-421 with u = 0, omega = 0).  Its sin / cos
 // are then exactly 0 / 1 and every yaw term drops out of the arithmetic.
+// The YAW0 flavour is also tilt-bounded: roll and pitch start every step
+// inside the +-pi/3 clamp (quadcopter_env.py:460-463; checked at kernel entry,
+// kept by every constrained step), so their sin / cos need no argument
+// reduction (sincos_tilt).
 template <bool YAW0 = false>
 __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 #pragma unroll
-  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) fast_sincos(ang[i], &t.s[i], &t.c[i]);
+  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
+    if (YAW0)
+      sincos_tilt(ang[i], &t.s[i], &t.c[i]);
+    else
+      fast_sincos(ang[i], &t.s[i], &t.c[i]);
+  }
   if (YAW0) t.s[2] = 0.0, t.c[2] = 1.0;
 }
 
@@ -419,13 +428,18 @@ __host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ct
 // needed: speed within 1e-14 of the clamp or above it, or an attitude angle
 // with (a + pi) outside (-2 pi, 4 pi), where numpy's floor-mod takes more
 // than one correction (or the state is not finite).
+// YAW0 (tilt-bounded, see trig_of): after an RK4 step from inside the tilt
+// clamp, |roll|, |pitch| <= pi/3 + small_angle_bound < pi, so a + pi lies in
+// (0, 2 pi) and numpy's floor-mod makes no correction: only the speed test
+// remains.
 template <bool YAW0 = false>
 __device__ __forceinline__ bool constrain_fast_ok(const qt_env_params& e, const double* x) {
   const double sv = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
   const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
   bool ok = sv < vm2;
+  if (YAW0) return ok;
 #pragma unroll
-  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
+  for (int i = 0; i < 3; ++i) {
     const double b = x[6 + i] + kPi;
     ok = ok & (b > -kTwoPi) & (b < 2.0 * kTwoPi);
   }
@@ -439,10 +453,11 @@ __device__ __forceinline__ void constrain_fast_apply(const qt_env_params& e, dou
 #pragma unroll
   for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
     // (b % 2 pi) for b in (-2 pi, 4 pi): one correction, the same rounding as
-    // numpy's (b < 0: b + 2 pi; b >= 2 pi: b - 2 pi, exact by Sterbenz)
+    // numpy's (b < 0: b + 2 pi; b >= 2 pi: b - 2 pi, exact by Sterbenz);
+    // YAW0: b in (0, 2 pi), none (constrain_fast_ok)
     const double b = x[6 + i] + kPi;
-    const double adj = b < 0.0 ? kTwoPi : (b >= kTwoPi ? -kTwoPi : 0.0);
-    x[6 + i] = (b + adj) - kPi;
+    const double adj = YAW0 ? 0.0 : (b < 0.0 ? kTwoPi : (b >= kTwoPi ? -kTwoPi : 0.0));
+    x[6 + i] = YAW0 ? b - kPi : (b + adj) - kPi;
   }
   x[6] = clip_num(x[6], -kMaxTilt, kMaxTilt);
   x[7] = clip_num(x[7], -kMaxTilt, kMaxTilt);

@@ -314,7 +314,9 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
                   isfinite(pl.inv_mass) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
   // structured gains never command yaw: a yaw at rest stays exactly zero
-  if (FLAVOR == kYaw0 || deferred == kYaw0) lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0;
+  // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>)
+  if (FLAVOR == kYaw0 || deferred == kYaw0)
+    lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0 && fabs(x[6]) <= kMaxTilt && fabs(x[7]) <= kMaxTilt;
   const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
   if (FLAVOR != kExact) {
     if (!wave_ok) return;

@@ -26,13 +26,16 @@ int main(int argc, char** argv) {
     double s, c;
     qt::fast_sincos(a, &s, &c);
     double m = qt::py_mod_2pi(a, 6.283185307179586);
-    double ss, cs;
+    double ss, cs, st, ct;
     qt::small_sincos(a, &ss, &cs);
+    qt::sincos_tilt(a, &st, &ct);
     fwrite(&s, 8, 1, o);
     fwrite(&c, 8, 1, o);
     fwrite(&m, 8, 1, o);
     fwrite(&ss, 8, 1, o);
     fwrite(&cs, 8, 1, o);
+    fwrite(&st, 8, 1, o);
+    fwrite(&ct, 8, 1, o);
   }
   fclose(o);
   return 0;
@@ -52,7 +55,7 @@ def probe(tmp_path_factory):
         x = np.ascontiguousarray(x, dtype=np.float64)
         (d / "in.bin").write_bytes(x.tobytes())
         subprocess.run([str(exe), str(d / "in.bin"), str(d / "out.bin")], check=True)
-        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 5)
+        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 7)
 
     return run
 
@@ -113,3 +116,16 @@ def test_angle_wrap_bit_identical_to_numpy(probe):
     same = (out == ref) | (np.isnan(out) & np.isnan(ref))
     assert np.all(same)
     assert not np.any(np.signbit(out[out == 0]))
+
+
+def test_tilt_sincos_accuracy(probe):
+    """sincos_tilt (no argument reduction) on the roll / pitch range of the
+    yaw-at-rest fast step: |a| <= pi/3 + 0.125."""
+    rng = np.random.default_rng(3)
+    lim = np.pi / 3 + 0.125
+    a = np.concatenate([rng.uniform(-lim, lim, 300000), [0.0, -0.0, 1e-300, np.pi / 3, -np.pi / 3, lim, -lim]])
+    out = probe(a)
+    st, ct = out[:, 5], out[:, 6]
+    assert np.max(ulp_err(st, np.sin(a))[np.abs(a) > 1e-300]) <= 1.0
+    assert np.max(ulp_err(ct, np.cos(a))) <= 2.0  # as fast_sincos: the last step 1 + z*q rounds at ulp(1)/2
+    assert st[300002] == 1e-300 and ct[300000] == 1.0 and st[300001] == 0.0
