@@ -208,7 +208,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       }
       a.sum_e += err;
       a.sum_e2 += err * err;
-      if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;  // np.max, NaN-propagating
+      if (FAST)  // err and max_e are numbers here (finite state): a plain max
+        a.max_e = fmax(a.max_e, err);
+      else if (!(err <= a.max_e) && !(a.max_e != a.max_e))
+        a.max_e = err;  // np.max, NaN-propagating
       const bool on = err <= R;
       a.on_pre += on;
       a.sum_u += un;
@@ -225,7 +228,12 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
       se_pre = se;
       const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
-      if (ok) {
+      // Wave-uniform choice: when any lane is off the fast preconditions the
+      // whole wave runs the exact code, which takes the fast code's decisions
+      // on the lanes that qualify.  A uniform, expected condition is a
+      // not-taken scalar branch with the exact code out of line; a divergent
+      // if / else cost a taken branch around the else block every step.
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
         a.on_post += se < er2lo;
       } else {  // rare: exact constraints and comparison

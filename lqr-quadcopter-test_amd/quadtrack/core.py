@@ -56,6 +56,16 @@ class EpisodeBatch:
         b.order = ptr(self.order)
         return b
 
+    def select(self, idx: torch.Tensor) -> "EpisodeBatch":
+        """The sub-batch of episodes `idx` (int64 on the device), in that order:
+        the same inputs column for column, runtime motion (no grouping)."""
+        idx = idx.to(device=self.device, dtype=torch.int64)
+        col = lambda t: None if t is None else t.index_select(-1, idx).contiguous()  # noqa: E731
+        K = self.K if self.K.shape[1] == 1 else col(self.K)
+        return EpisodeBatch(n=idx.numel(), device=self.device, pattern=col(self.pattern), offset=col(self.offset), K=K,
+                            k_cols=self.k_cols, motion=col(self.motion), plant_mass=col(self.plant_mass),
+                            hover=col(self.hover), k_structured=self.k_structured)
+
 
 @dataclass
 class RolloutState:

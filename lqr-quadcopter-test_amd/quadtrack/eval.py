@@ -23,6 +23,7 @@ from typing import Callable
 
 import numpy as np
 
+from ._abi import MET
 from .controllers import (
     BaseController,
     LQRController,
@@ -153,11 +154,7 @@ def evaluate_batched(controller, env_config=None, num_episodes: int = 10, base_s
     BatchedLQR, BatchedPID: shared or per-episode gains) or a config dict
     (its "controller" key picks the type, default riccati_lqr)."""
     cfg = as_env_config(env_config)
-    if isinstance(controller, dict):
-        c = dict(controller)
-        controller = batched_controller(c.pop("controller", "riccati_lqr"), c)
-    elif isinstance(controller, (RiccatiLQRController, LQRController, PIDController)):
-        controller = controller.to_batched()
+    controller = _as_batched(controller)
     seeds = base_seed + global_offset + np.arange(num_episodes)
     res = run_closed_loop(controller, cfg, n=num_episodes, seeds=seeds, motion=motion, plant_mass=plant_mass,
                           criteria=criteria, max_steps=max_steps_per_episode)
@@ -165,3 +162,84 @@ def evaluate_batched(controller, env_config=None, num_episodes: int = 10, base_s
     if with_episode_metrics:
         summary.episode_metrics = res.episode_metrics()
     return summary
+
+
+def _as_batched(controller):
+    if isinstance(controller, dict):
+        c = dict(controller)
+        return batched_controller(c.pop("controller", "riccati_lqr"), c)
+    if isinstance(controller, (RiccatiLQRController, LQRController, PIDController)):
+        return controller.to_batched()
+    return controller
+
+
+class BatchedEvaluator:
+    """The Evaluator pipeline (eval.py:59-268) with every episode in one fused
+    launch and a fresh controller per episode (the tuner / trainer semantics,
+    SURVEY F8).  `evaluate` fills `episode_data_list` / `episode_info_list` in
+    the reference's formats (eval.py:142-158, the env's final info dict,
+    quadcopter_env.py:209-226) for the episodes in `record_episodes` (default:
+    all of them up to 64), recorded by a re-run of just those episodes."""
+
+    def __init__(self, controller, env_config=None, criteria: SuccessCriteria | None = None,
+                 output_dir: str | Path = "reports"):
+        self.controller = controller
+        self.env_config = as_env_config(env_config)
+        self.criteria = criteria or SuccessCriteria()
+        self.output_dir = Path(output_dir)
+        self.output_dir.mkdir(parents=True, exist_ok=True)
+        self.episode_data_list: list[list[dict]] = []
+        self.episode_info_list: list[dict] = []
+        self.result = None
+
+    def evaluate(self, num_episodes: int = 10, base_seed: int = 42, max_steps_per_episode: int | None = None,
+                 verbose: bool = True, record_episodes=None, group=None, global_offset: int = 0) -> EvaluationSummary:
+        seeds = base_seed + global_offset + np.arange(num_episodes)
+        res = run_closed_loop(_as_batched(self.controller), self.env_config, n=num_episodes, seeds=seeds,
+                              criteria=self.criteria, max_steps=max_steps_per_episode)
+        self.result = res
+        if record_episodes is None:
+            record_episodes = range(num_episodes) if num_episodes <= 64 else []
+        rec = [int(i) for i in record_episodes]
+        self.episode_data_list = res.episode_data(rec) if rec else []
+        self.episode_info_list = self._final_info(res, rec, self.episode_data_list) if rec else []
+        summary = res.summary(group=group, global_offset=global_offset)
+        summary.episode_metrics = res.episode_metrics()
+        if verbose:
+            print("\n" + format_metrics_report(summary))
+        return summary
+
+    def _final_info(self, res, episodes, data) -> list[dict]:
+        """The info dict env.step returned on each episode's last step."""
+        from ._abi import TERM_REASONS
+
+        met = res.metrics.cpu().numpy()
+        env = res.env
+        out = []
+        for j, e in enumerate(episodes):
+            steps = int(met[MET["steps"], e])
+            if steps == 0:
+                out.append({})
+                continue
+            last = data[j][-1]
+            ratio = float(met[MET["env_on_target_ratio"], e])
+            info = {"time": last["time"], "step": steps, "tracking_error": last["tracking_error"],
+                    "on_target": last["on_target"], "on_target_ratio": ratio,
+                    "action_violations": int(met[MET["action_violations"], e])}
+            term = int(met[MET["termination_code"], e])
+            if term:
+                info["termination_reason"] = TERM_REASONS[term]
+                info["episode_length"] = last["time"]
+                info["success"] = bool(last["time"] >= env.min_episode_duration and ratio >= env.min_on_target_ratio)
+            out.append(info)
+        return out
+
+    def save_report(self, summary: EvaluationSummary, experiment_name: str | None = None) -> dict[str, Path]:
+        """metrics.json + text report (eval.py:233-268)."""
+        if experiment_name is None:
+            stamp = datetime.now(timezone.utc).strftime("%Y%m%d_%H%M%S")
+            experiment_name = f"eval_{getattr(self.controller, 'name', 'batched')}_{stamp}"
+        paths = {"metrics": self.output_dir / "metrics.json", "report": self.output_dir / f"{experiment_name}_report.txt"}
+        paths["metrics"].write_text(json.dumps(summary.to_dict(), indent=2))
+        paths["report"].write_text(format_metrics_report(summary))
+        return paths

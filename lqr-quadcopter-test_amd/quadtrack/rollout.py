@@ -42,7 +42,9 @@ class RolloutResult:
     state: core.RolloutState
     batch: core.EpisodeBatch
     criteria: object
-    record: torch.Tensor | None = None  # [steps, 16, n]: state after step + applied action
+    record: torch.Tensor | None = None  # [steps, 16, n]: state after step + controller command
+    env: object = None                  # EnvParams of the run (trajectory re-runs)
+    ctrl: object = None                 # CtrlParams of the run
 
     @property
     def n(self) -> int:
@@ -80,6 +82,136 @@ class RolloutResult:
         from .parallel import reduce_summary
 
         return reduce_summary(self.metrics, self.criteria, group=group, global_offset=global_offset)
+
+    # ------------------------------------------------------------ trajectories
+    def trajectories(self, episodes=None) -> dict:
+        """Per-step arrays of the selected episodes (default: all), for plots and
+        reports in the reference's step-record layouts (eval.py:142-158,
+        quadcopter_env.py:555-584).
+
+        The fused rollout keeps no per-step data, so the selected episodes are
+        re-run from their own inputs with recording on (the exact step: the same
+        decisions as the fast step, values equal to ~1e-9).  m = len(episodes),
+        S = the longest executed episode among them:
+
+          time            [S]        post-step time (info["time"]; t accumulates dt)
+          obs_state       [S, 12, m] state the action was computed on (pre-step)
+          obs_target      [S, 9, m]  target observation (p, v, a) at that time
+          next_state      [S, 12, m] state after the step
+          next_target     [S, 9, m]  target observation after the step
+          action          [S, 4, m]  controller command (thrust, roll, pitch, yaw rate)
+          applied         [S, 4, m]  command after the env's action parsing (quadcopter_env.py:234-293)
+          tracking_error  [S, m]     post-step ‖p − p_T‖ (quadcopter_env.py:498-502); reward = −error
+          on_target       [S, m]     bool, error <= the env's target radius
+          steps           [m]        executed steps; rows at or beyond them are NaN / False
+        """
+        if self.env is None or self.ctrl is None:
+            raise ValueError("trajectories need the run's env and controller parameters (run_closed_loop)")
+        dev = self.batch.device
+        if episodes is None:
+            idx = torch.arange(self.n, device=dev)
+        else:
+            idx = torch.as_tensor(np.asarray(episodes, dtype=np.int64).reshape(-1), device=dev)
+        if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= self.n):
+            raise IndexError(f"episode index out of range for {self.n} episodes")
+        env, m = self.env, idx.numel()
+        steps = self.metrics[MET["steps"]].index_select(0, idx).to(torch.int64)
+        S = int(steps.max().item()) if m else 0
+        nan = float("nan")
+        rec = torch.full((S, 16, m), nan, dtype=F64, device=dev)
+        st = core.RolloutState.empty(m, dev)
+        sub = self.batch.select(idx)
+        if m:
+            core.reset(env, sub, st)
+        x0 = st.x.clone()
+        if S and m:
+            core.rollout(env, self.ctrl, self.criteria, sub, st, S, rec)
+        times = np.concatenate([[0.0], np.cumsum(np.full(S, env.dt))])  # t_0 .. t_S, sequential t += dt
+        tg = _targets_at(env, sub, torch.as_tensor(times, dtype=F64, device=dev))  # [S + 1, 9, m]
+        valid = torch.arange(S, device=dev)[:, None] < steps[None, :]
+        obs_state = torch.cat([x0[None], rec[:-1, :12]]) if S else rec[:, :12]
+        nxt = rec[:, :12]
+        d = nxt[:, 0:3] - tg[1:, 0:3]
+        err = torch.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1] + d[:, 2] * d[:, 2])
+        act = rec[:, 12:16]
+        applied = torch.nan_to_num(act, nan=0.0, posinf=0.0, neginf=0.0)
+        applied[:, 0].clamp_(env.min_thrust, env.max_thrust)
+        applied[:, 1:].clamp_(-env.max_angular_rate, env.max_angular_rate)
+        v3 = valid[:, None, :]
+        mask = lambda a, v: torch.where(v, a, torch.full_like(a, nan))  # noqa: E731
+        return {
+            "time": torch.as_tensor(times[1:], dtype=F64, device=dev),
+            "obs_state": mask(obs_state, v3), "obs_target": mask(tg[:-1], v3),
+            "next_state": mask(nxt, v3), "next_target": mask(tg[1:], v3),
+            "action": mask(act, v3), "applied": mask(applied, v3),
+            "tracking_error": mask(err, valid), "on_target": (err <= env.target_radius) & valid,
+            "steps": steps,
+        }
+
+    def episode_data(self, episodes=None) -> list[list[dict]]:
+        """The Evaluator's step records of each selected episode (eval.py:142-158):
+        pre-step observation, controller command, post-step time / reward /
+        tracking error / on-target flag."""
+        tr = {k: v.cpu().numpy() for k, v in self.trajectories(episodes).items()}
+        out = []
+        for j in range(tr["steps"].size):
+            rows = []
+            for k in range(int(tr["steps"][j])):
+                qs, ts = tr["obs_state"][k, :, j], tr["obs_target"][k, :, j]
+                rows.append({
+                    "time": float(tr["time"][k]), "step": k,
+                    "quadcopter_position": qs[0:3].tolist(), "quadcopter_velocity": qs[3:6].tolist(),
+                    "target_position": ts[0:3].tolist(), "target_velocity": ts[3:6].tolist(),
+                    "action": tr["action"][k, :, j].tolist(),
+                    "reward": -float(tr["tracking_error"][k, j]),
+                    "tracking_error": float(tr["tracking_error"][k, j]),
+                    "on_target": bool(tr["on_target"][k, j]),
+                })
+            out.append(rows)
+        return out
+
+    def history(self, episodes=None, log_interval: int = 10) -> list[list[dict]]:
+        """QuadcopterEnv.get_history() of each selected episode
+        (quadcopter_env.py:555-584): the steps whose post-step count is a multiple
+        of log_interval, with the post-step observation and the applied action."""
+        if log_interval < 1:
+            raise ValueError("log_interval must be >= 1")
+        tr = {k: v.cpu().numpy() for k, v in self.trajectories(episodes).items()}
+        out = []
+        for j in range(tr["steps"].size):
+            rows = []
+            for k in range(log_interval - 1, int(tr["steps"][j]), log_interval):
+                qs, ts = tr["next_state"][k, :, j], tr["next_target"][k, :, j]
+                rows.append({
+                    "time": float(tr["time"][k]), "step": k + 1,
+                    "quadcopter_position": qs[0:3].tolist(), "quadcopter_velocity": qs[3:6].tolist(),
+                    "quadcopter_attitude": qs[6:9].tolist(),
+                    "target_position": ts[0:3].tolist(), "target_velocity": ts[3:6].tolist(),
+                    "action": tr["applied"][k, :, j].tolist(),
+                    "reward": -float(tr["tracking_error"][k, j]),
+                    "tracking_error": float(tr["tracking_error"][k, j]),
+                    "on_target": bool(tr["on_target"][k, j]),
+                })
+            out.append(rows)
+        return out
+
+
+def _targets_at(env, batch: core.EpisodeBatch, times: torch.Tensor) -> torch.Tensor:
+    """Target observation of every episode of `batch` at every time -> [T, 9, m]
+    (qt_target_state on a time-major replicated batch, ~4 M evaluations per launch)."""
+    T, m, dev = times.numel(), batch.n, batch.device
+    out = torch.empty(T, 9, m, dtype=F64, device=dev)
+    if T == 0 or m == 0:
+        return out
+    rows = max(1, (1 << 22) // m)
+    for lo in range(0, T, rows):
+        k = min(rows, T - lo)
+        rep = core.EpisodeBatch(n=k * m, device=dev, pattern=batch.pattern.repeat(1, k),
+                                offset=batch.offset.repeat(1, k), K=batch.K[:, :1], k_cols=batch.k_cols,
+                                motion=None if batch.motion is None else batch.motion.repeat(k))
+        tg = core.target_state(env, rep, times[lo:lo + k].repeat_interleave(m).contiguous())
+        out[lo:lo + k] = tg.view(9, k, m).permute(1, 0, 2)
+    return out
 
 
 def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, motion=None, plant_mass=None,
@@ -150,7 +282,8 @@ def run_closed_loop(controller: BatchedRiccatiLQR, env_config=None, n: int | Non
         core.rollout(env, controller.ctrl, crit, batch, st, k, None if rec is None else rec[done:done + k])
         done += k
     met = core.episode_metrics(crit, st)
-    return RolloutResult(metrics=met, state=st, batch=batch, criteria=crit, record=rec)
+    return RolloutResult(metrics=met, state=st, batch=batch, criteria=crit, record=rec, env=env,
+                         ctrl=controller.ctrl)
 
 
 def _criteria(criteria):

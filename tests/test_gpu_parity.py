@@ -598,3 +598,51 @@ def test_evaluate_batched_vs_evaluator_pid_lqr(qt, kind):
     bat = evaluate_batched(ctl, cfg, num_episodes=3, base_seed=7)
     for k in ("mean_on_target_ratio", "mean_tracking_error", "std_tracking_error", "mean_control_effort"):
         assert getattr(bat, k) == pytest.approx(getattr(seq, k), rel=1e-9, abs=1e-12), k
+
+
+def _same_records(got, ref, vec_keys):
+    assert len(got) == len(ref)
+    for b, a in zip(got, ref):
+        assert set(b) == set(a)
+        assert b["step"] == a["step"] and bool(b["on_target"]) == bool(a["on_target"])
+        for k in ("time", "reward", "tracking_error"):
+            assert b[k] == pytest.approx(a[k], rel=1e-9, abs=1e-12), k
+        for k in vec_keys:
+            np.testing.assert_allclose(b[k], a[k], rtol=1e-9, atol=1e-12, err_msg=k)
+
+
+@pytest.mark.parametrize("motion", ["circular", "figure8"])
+def test_trajectory_records_match_sequential(qt, motion):
+    """Step records from the batched path (BatchedEvaluator.episode_data_list,
+    RolloutResult.history) == the drop-in Evaluator's episode_data_list /
+    episode_info_list and the drop-in env's get_history(), stepped one step at a
+    time (eval.py:142-158, quadcopter_env.py:209-226, 555-584)."""
+    import tempfile
+
+    from quadtrack import BatchedEvaluator, Evaluator, QuadcopterEnv, RiccatiLQRController
+    from quadtrack.env import EnvConfig
+
+    cfg = EnvConfig.from_dict({"target": {"motion_type": motion}, "simulation": {"max_episode_time": 1.5},
+                               "logging": {"enabled": True, "log_interval": 7}})
+    ctl = RiccatiLQRController({"dt": 0.01})
+    with tempfile.TemporaryDirectory() as d:
+        seq = Evaluator(ctl, cfg, output_dir=d)
+        seq.evaluate(num_episodes=3, base_seed=5, verbose=False)
+        bat = BatchedEvaluator(ctl, cfg, output_dir=d)
+        bat.evaluate(num_episodes=3, base_seed=5, verbose=False)
+    keys = ("quadcopter_position", "quadcopter_velocity", "target_position", "target_velocity", "action")
+    assert len(bat.episode_data_list) == 3
+    for got, ref in zip(bat.episode_data_list, seq.episode_data_list):
+        _same_records(got, ref, keys)
+    for b, a in zip(bat.episode_info_list, seq.episode_info_list):
+        assert set(b) == set(a)
+        for k in a:
+            if isinstance(a[k], float):
+                assert b[k] == pytest.approx(a[k], rel=1e-9, abs=1e-12), k
+            else:
+                assert b[k] == a[k], k
+    env = QuadcopterEnv(cfg)
+    obs, done, c = env.reset(seed=6), False, RiccatiLQRController({"dt": 0.01})
+    while not done:
+        obs, _, done, _ = env.step(c.compute_action(obs))
+    _same_records(bat.result.history([1], log_interval=7)[0], env.get_history(), keys + ("quadcopter_attitude",))
