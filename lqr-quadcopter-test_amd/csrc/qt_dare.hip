@@ -586,8 +586,9 @@ __global__ __launch_bounds__(kDenseThreads) void dare_dense_kernel(int n, int p,
 extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gravity, const double* mass,
                                const double* q, const double* r, int32_t structured, double* K, double* P,
                                int8_t* status, int32_t* iters, void* stream) {
-  if ((n_state != 6 && n_state != 9) || m < 0 || !q || !r || !K || !status) return QT_EINVAL;
-  if (m == 0) return QT_OK;
+  if ((n_state != 6 && n_state != 9) || m < 0) return QT_EINVAL;
+  if (m == 0) return QT_OK;  // empty: no pointer is read
+  if (!q || !r || !K || !status) return QT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (structured) {
     const int64_t lanes = 4 * m;
@@ -607,9 +608,9 @@ extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gra
 extern "C" int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, const double* B,
                              int32_t ab_per_problem, const double* q, const double* r, double* K, double* P,
                              int8_t* status, int32_t* iters, void* stream) {
-  if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > 0x7fffffff || !A || !B || !q || !r || !K || !status)
-    return QT_EINVAL;
-  if (m == 0) return QT_OK;
+  if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > 0x7fffffff) return QT_EINVAL;
+  if (m == 0) return QT_OK;  // empty: no pointer is read
+  if (!A || !B || !q || !r || !K || !status) return QT_EINVAL;
   dare_dense_kernel<<<(int)m, kDenseThreads, 0, (hipStream_t)stream>>>(n, p, m, A, B, ab_per_problem, 0.0, 0.0,
                                                                        nullptr, q, r, 0, K, P, status, iters);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;

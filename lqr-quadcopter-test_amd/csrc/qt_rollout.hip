@@ -754,8 +754,9 @@ extern "C" {
 int qt_abi_version(void) { return QT_ABI_VERSION; }
 
 int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, qt_state st, void* stream) {
-  if (!env || !batch || !offset || batch->n < 0 || !valid_state(st, false)) return QT_EINVAL;
-  if (batch->n == 0) return QT_OK;
+  if (!env || !batch || batch->n < 0) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;  // empty: no per-episode pointer is read
+  if (!offset || !valid_state(st, false)) return QT_EINVAL;
   reset_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), offset, st);
   return check_launch();
 }
@@ -764,8 +765,8 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
                qt_state st, int32_t nsteps, double* rec, void* stream) {
   if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
   if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (batch->n == 0 || nsteps == 0) return QT_OK;  // nothing to run: no per-episode pointer is read
   if (!valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
-  if (batch->n == 0 || nsteps == 0) return QT_OK;
   const BatchDev b = to_dev(batch);
   const int grid = grid_of(batch->n);
   const int motion = batch->motion ? -1 : env->motion;
@@ -786,7 +787,7 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream) {
   if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
   if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
-  if (!valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
+  if (batch->n > 0 && nsteps > 0 && !valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
   if (nseg < 0 || (nseg > 0 && (!seg_motion || !seg_end))) return QT_EINVAL;
   int64_t prev = 0;
   for (int32_t i = 0; i < nseg; ++i) {
@@ -817,8 +818,9 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
 
 int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action, qt_state st, double* err,
                 int8_t* on_target, int8_t* done, int8_t* term, int8_t* violation, void* stream) {
-  if (!env || !batch || !action || batch->n < 0 || !valid_state(st, false)) return QT_EINVAL;
+  if (!env || !batch || batch->n < 0) return QT_EINVAL;
   if (batch->n == 0) return QT_OK;
+  if (!action || !valid_state(st, false)) return QT_EINVAL;
   env_step_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), action, st, err,
                                                                          on_target, done, term, violation);
   return check_launch();
@@ -826,10 +828,10 @@ int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* a
 
 int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs, double* integ,
                       double* action, int8_t* saturated, double* diag, void* stream) {
-  if (!ctrl || !batch || !obs || !action || !batch->K || batch->n < 0) return QT_EINVAL;
+  if (!ctrl || !batch || !batch->K || batch->n < 0) return QT_EINVAL;
   if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
-  if (batch->k_cols != 6 && !integ) return QT_EINVAL;
   if (batch->n == 0) return QT_OK;
+  if (!obs || !action || (batch->k_cols != 6 && !integ)) return QT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (batch->k_cols == 9)
     action_kernel<9><<<grid_of(batch->n), kBlock, 0, s>>>(*ctrl, to_dev(batch), obs, integ, action, saturated, diag);
@@ -841,16 +843,18 @@ int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const d
 }
 
 int qt_target_state(const qt_env_params* env, const qt_batch* batch, const double* t, double* out, void* stream) {
-  if (!env || !batch || !t || !out || batch->n < 0) return QT_EINVAL;
+  if (!env || !batch || batch->n < 0) return QT_EINVAL;
   if (batch->n == 0) return QT_OK;
+  if (!t || !out) return QT_EINVAL;
   target_kernel<<<grid_of(batch->n), kBlock, 0, (hipStream_t)stream>>>(*env, to_dev(batch), t, out);
   return check_launch();
 }
 
 int qt_episode_metrics(const qt_criteria* crit, int64_t n, const double* acc, const double* t, double* met,
                        void* stream) {
-  if (!crit || !acc || !t || !met || n < 0) return QT_EINVAL;
+  if (!crit || n < 0) return QT_EINVAL;
   if (n == 0) return QT_OK;
+  if (!acc || !t || !met) return QT_EINVAL;
   metrics_kernel<<<grid_of(n), kBlock, 0, (hipStream_t)stream>>>(*crit, n, acc, t, met);
   return check_launch();
 }
@@ -858,23 +862,23 @@ int qt_episode_metrics(const qt_criteria* crit, int64_t n, const double* acc, co
 int qt_metrics_from_arrays(const qt_criteria* crit, int64_t n, int32_t max_steps, const double* qpos,
                            const double* tpos, const double* actions, const int32_t* steps,
                            const double* last_time, double* met, void* stream) {
-  if (!crit || n < 0 || max_steps < 0 || !steps || !last_time || !met) return QT_EINVAL;
-  if (max_steps > 0 && (!qpos || !tpos || !actions)) return QT_EINVAL;
+  if (!crit || n < 0 || max_steps < 0) return QT_EINVAL;
   if (n == 0) return QT_OK;
+  if (!steps || !last_time || !met || (max_steps > 0 && (!qpos || !tpos || !actions))) return QT_EINVAL;
   metrics_arrays_kernel<<<grid_of(n), kBlock, 0, (hipStream_t)stream>>>(*crit, n, max_steps, qpos, tpos, actions,
                                                                         steps, last_time, met);
   return check_launch();
 }
 
 int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, void* stream) {
-  if (!met || !out || n < 0) return QT_EINVAL;
+  if (!out || n < 0 || (n > 0 && !met)) return QT_EINVAL;  // n == 0: writes the empty partial
   summary_kernel<<<1, kSumBlock, 0, (hipStream_t)stream>>>(n, met, mu_ratio, mu_err, out);
   return check_launch();
 }
 
 int qt_summary_parts(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, double* work,
                      int32_t nparts, void* stream) {
-  if (!met || !out || !work || n < 0 || nparts < 1 || nparts > 4096) return QT_EINVAL;
+  if (!out || !work || n < 0 || (n > 0 && !met) || nparts < 1 || nparts > 4096) return QT_EINVAL;
   const int64_t chunk = (n + nparts - 1) / nparts > 0 ? (n + nparts - 1) / nparts : 1;
   hipStream_t s = (hipStream_t)stream;
   summary_part_kernel<<<nparts, kSumBlock, 0, s>>>(n, met, mu_ratio, mu_err, chunk, work);

@@ -61,16 +61,18 @@ __global__ __launch_bounds__(256) void seed_uniform_kernel(int64_t n, const int6
 
 extern "C" int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo, const double* hi,
                                double* out, void* stream) {
-  if (n < 0 || k < 0 || k > 64 || !seeds || !lo || !hi || !out) return QT_EINVAL;
-  if (n == 0 || k == 0) return QT_OK;
+  if (n < 0 || k < 0 || k > 64) return QT_EINVAL;
+  if (n == 0 || k == 0) return QT_OK;  // empty: no pointer is read
+  if (!seeds || !lo || !hi || !out) return QT_EINVAL;
   seed_uniform_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(n, seeds, k, lo, hi, out);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }
 
 extern "C" int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t motion_default,
                              double* pattern, double* offset, void* stream) {
-  if (n < 0 || !seeds || !pattern || !offset || motion_default < 0 || motion_default > 4) return QT_EINVAL;
-  if (n == 0) return QT_OK;
+  if (n < 0 || motion_default < 0 || motion_default > 4) return QT_EINVAL;
+  if (n == 0) return QT_OK;  // empty: no pointer is read
+  if (!seeds || !pattern || !offset) return QT_EINVAL;
   seed_draws_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(n, seeds, motion, motion_default,
                                                                               pattern, offset);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;

@@ -147,6 +147,58 @@ def test_full_batch_65536_linear_vs_oracle(qt):
     np.testing.assert_allclose(res.state.x.cpu().numpy()[:, sample].T, oxf, rtol=1e-8, atol=TOL)
 
 
+def _oracle_batch(env_cfg, motion, seeds, max_steps=-1):
+    env = O.env_params(env_cfg)
+    c, K, kc, _, _ = O.controller({"dt": 0.01})
+    pat, off = O.draws(motion, seeds)
+    x0 = np.array([O.initial_state(env, env.motion, pat[i], off[i]) for i in range(len(seeds))]).reshape(-1, 12)
+    om, oxf, _, _ = O.rollout(env, c, O.criteria(), None, pat.reshape(-1, 4), None, None, K, kc, False, x0,
+                              max_steps=max_steps)
+    return om, oxf
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 257])
+def test_empty_and_ragged_batches(qt, n):
+    """Batch sizes that are not a multiple of the wave (64) or workgroup (256),
+    and the empty batch, through the same launchers; 400 steps vs the oracle."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    cfg = {"target": {"motion_type": "circular"}}
+    seeds = np.arange(1000, 1000 + n)
+    res = run_closed_loop(BatchedRiccatiLQR({"dt": 0.01}), cfg, n=n, seeds=seeds, max_steps=400)
+    assert tuple(res.metrics.shape) == (len(FIELDS), n)
+    if n == 0:
+        assert res.summary().total_episodes == 0
+        return
+    om, oxf = _oracle_batch(cfg, "circular", seeds, max_steps=400)
+    np.testing.assert_allclose(res.metrics.cpu().numpy().T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(res.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=TOL)
+
+
+def test_position_bounds_termination_mid_wave(qt):
+    """Lanes of one wavefront leaving the position bounds at different steps
+    (a 3 m/s linear target, max_position 4 m): per-lane termination step and
+    reason vs the oracle, and the fast step (divergent early exit) vs the
+    exact step."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = 512
+    cfg = {"target": {"motion_type": "linear", "speed": 3.0}, "simulation": {"max_position": 4.0}}
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    fast = run_closed_loop(ctl, cfg, n=n, seeds=np.arange(n))
+    exact = run_closed_loop(ctl, cfg, n=n, seeds=np.arange(n), record=True)
+    mf = fast.metrics.cpu().numpy()
+    steps, term = mf[FIELDS.index("steps")], mf[FIELDS.index("termination_code")]
+    assert np.all(term == 2) and len(np.unique(steps)) > 20  # position_bounds, at many different steps
+    np.testing.assert_array_equal(mf[FIELDS.index("steps")], exact.metrics.cpu().numpy()[FIELDS.index("steps")])
+    np.testing.assert_allclose(mf, exact.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    om, oxf = _oracle_batch(cfg, "linear", np.arange(n))
+    np.testing.assert_allclose(mf.T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=TOL)
+
+
 def test_chunked_equals_single_launch(qt):
     """Idempotence of chunking: 3000 steps in one launch == 7 uneven chunks."""
     from quadtrack.controllers import BatchedRiccatiLQR
