@@ -200,6 +200,8 @@ __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 // with sin d / cos d from small_sincos.  The stage offsets are h * (body rate)
 // <= dt * ~12 rad/s; an offset beyond the polynomial's range takes fast_sincos.
 // SMALL: the caller has proven |delta| <= kSmallAngle (small_angle_bound).
+// YAW0 (the yaw-at-rest flavour, which is also rate-bounded: rate_bounded_ok)
+// has |delta| <= kRateAngle and takes the shorter rate_sincos.
 template <bool SMALL = false, bool YAW0 = false>
 __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t) {
   constexpr int NA = YAW0 ? 2 : 3;
@@ -208,7 +210,10 @@ __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, co
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       double sd, cd;
-      small_sincos(delta[i], &sd, &cd);
+      if (YAW0)
+        rate_sincos(delta[i], &sd, &cd);
+      else
+        small_sincos(delta[i], &sd, &cd);
       t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
       t.c[i] = fma(t0.c[i], cd, -(t0.s[i] * sd));
     }
@@ -421,6 +426,20 @@ __host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ct
   return e.integrator == 0 && c.min_thrust >= e.min_thrust && c.max_thrust <= e.max_thrust &&
          c.min_thrust <= c.max_thrust && c.max_rate <= e.max_angular_rate && c.max_rate >= 0.0 &&
          e.max_angular_velocity >= 0.0 && small_angle_bound(e) <= kSmallAngle;
+}
+
+// Rate-bounded steps (the yaw-at-rest flavour's third precondition).  The
+// body-rate dynamics are linear, w' = 10 (u - w) - c w with the command u
+// constant over the step and |u| <= max_rate (the controller's clip).  With
+// c >= 0 and dt (10 + c) <= 1 every RK4 stage rate is a combination of w and u
+// with non-negative weights summing to at most 1 (stage 2: (1 - a) w + b u,
+// a = dt / 2 (10 + c), b = 5 dt; stages 3, 4 and the update likewise), so a
+// lane whose |w| starts within max_rate keeps every stage rate, and the next
+// step's rate, within max_rate (the rate clamp only shrinks it).  A stage
+// attitude offset h * w (h <= dt) is then at most dt * max_rate <= kRateAngle.
+__host__ __device__ inline bool rate_bounded_ok(const qt_env_params& e, const qt_ctrl_params& c) {
+  return c.max_rate >= 0.0 && e.drag_angular >= 0.0 && e.dt > 0.0 && e.dt * (10.0 + e.drag_angular) <= 1.0 &&
+         e.dt * c.max_rate * (1.0 + 1e-9) <= kRateAngle;
 }
 
 // Fast-path state constraints: the common case of _apply_state_constraints

@@ -83,15 +83,15 @@ QT_HD void small_sincos(double d, double* s, double* c) {
   *c = fma(z, q, 1.0);
 }
 
-// sin / cos of an attitude inside the tilt clamp, |a| <= pi/3 + 0.125
-// (roll / pitch of the fast step: clamped to +-pi/3 every step, so a step
-// starts inside it), without argument reduction or quadrant selects: Taylor
-// polynomials to a^19 / a^20, whose truncation error is below 1e-19 there;
-// <= 1 ulp (sin) / 2 ulp (cos: its last step 1 + z q rounds at ulp(1) / 2).
+// sin / cos of an attitude inside the tilt clamp, |a| <= pi/3 (roll / pitch
+// at the start of a fast step: clamped to +-pi/3 every step, checked at
+// kernel entry), without argument reduction or quadrant selects: Taylor
+// polynomials to a^17 / a^18, whose truncation error is below 2e-17 (sin,
+// the a^19 / 19! term) and 1.1e-18 (cos) there; <= 1 ulp (sin) / 2 ulp (cos:
+// its last step 1 + z q rounds at ulp(1) / 2).
 QT_HD void sincos_tilt(double a, double* s, double* c) {
   const double z = a * a;
-  double p = -8.22063524662433e-18;      // -1/19!
-  p = fma(z, p, 2.8114572543455206e-15);  // 1/17!
+  double p = 2.8114572543455206e-15;      // 1/17!
   p = fma(z, p, -7.647163731819816e-13);  // -1/15!
   p = fma(z, p, 1.6059043836821613e-10);  // 1/13!
   p = fma(z, p, -2.505210838544172e-08);  // -1/11!
@@ -100,14 +100,30 @@ QT_HD void sincos_tilt(double a, double* s, double* c) {
   p = fma(z, p, 8.3333333333333332e-03);  // 1/5!
   p = fma(z, p, -1.6666666666666666e-01);  // -1/3!
   *s = fma(a * z, p, a);
-  double q = 4.110317623312165e-19;       // 1/20!
-  q = fma(z, q, -1.5619206968586225e-16);  // -1/18!
+  double q = -1.5619206968586225e-16;     // -1/18!
   q = fma(z, q, 4.779477332387385e-14);   // 1/16!
   q = fma(z, q, -1.1470745597729725e-11);  // -1/14!
   q = fma(z, q, 2.08767569878681e-09);    // 1/12!
   q = fma(z, q, -2.7557319223985888e-07);  // -1/10!
   q = fma(z, q, 2.4801587301587302e-05);  // 1/8!
   q = fma(z, q, -1.3888888888888889e-03);  // -1/6!
+  q = fma(z, q, 4.1666666666666664e-02);  // 1/4!
+  q = fma(z, q, -0.5);
+  *c = fma(z, q, 1.0);
+}
+
+// sin / cos of an RK4 stage offset of a rate-bounded step, |d| <= kRateAngle
+// (dt * max commanded rate: 0.03 at the defaults): Taylor polynomials to d^7 /
+// d^6, truncation below 8e-20 (sin) and 2.2e-17 (cos, the d^8 / 8! term).
+constexpr double kRateAngle = 0.031;
+
+QT_HD void rate_sincos(double d, double* s, double* c) {
+  const double z = d * d;
+  double p = -1.9841269841269841e-04;     // -1/7!
+  p = fma(z, p, 8.3333333333333332e-03);  // 1/5!
+  p = fma(z, p, -1.6666666666666666e-01);  // -1/3!
+  *s = fma(d * z, p, d);
+  double q = -1.3888888888888889e-03;     // -1/6!
   q = fma(z, q, 4.1666666666666664e-02);  // 1/4!
   q = fma(z, q, -0.5);
   *c = fma(z, q, 1.0);

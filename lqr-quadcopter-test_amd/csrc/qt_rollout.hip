@@ -322,9 +322,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
                   isfinite(pl.inv_mass) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
   // structured gains never command yaw: a yaw at rest stays exactly zero
-  // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>)
+  // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
+  // rate-bounded, roll and pitch rates within the command clip: rate_bounded_ok)
   if (FLAVOR == kYaw0 || deferred == kYaw0)
-    lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0 && fabs(x[6]) <= kMaxTilt && fabs(x[7]) <= kMaxTilt;
+    lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0 && fabs(x[6]) <= kMaxTilt && fabs(x[7]) <= kMaxTilt &&
+              fabs(x[9]) <= c.max_rate && fabs(x[10]) <= c.max_rate;
   const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
   if (FLAVOR != kExact) {
     if (!wave_ok) return;
@@ -686,10 +688,12 @@ int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH
 template <int MOTION, int KC, bool FF, bool KS>
 void launch_flavours(bool fast, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                      const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
-  constexpr int kF = KS ? kYaw0 : kFast;
-  if (fast) {
-    rollout_kernel<kF, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kF);
+  if (fast && KS && rate_bounded_ok(e, c)) {
+    rollout_kernel<kYaw0, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kYaw0);
+  } else if (fast) {
+    rollout_kernel<kFast, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kFast);
   } else {
     rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
   }

@@ -26,9 +26,10 @@ int main(int argc, char** argv) {
     double s, c;
     qt::fast_sincos(a, &s, &c);
     double m = qt::py_mod_2pi(a, 6.283185307179586);
-    double ss, cs, st, ct;
+    double ss, cs, st, ct, sr, cr;
     qt::small_sincos(a, &ss, &cs);
     qt::sincos_tilt(a, &st, &ct);
+    qt::rate_sincos(a, &sr, &cr);
     fwrite(&s, 8, 1, o);
     fwrite(&c, 8, 1, o);
     fwrite(&m, 8, 1, o);
@@ -36,6 +37,8 @@ int main(int argc, char** argv) {
     fwrite(&cs, 8, 1, o);
     fwrite(&st, 8, 1, o);
     fwrite(&ct, 8, 1, o);
+    fwrite(&sr, 8, 1, o);
+    fwrite(&cr, 8, 1, o);
   }
   fclose(o);
   return 0;
@@ -55,7 +58,7 @@ def probe(tmp_path_factory):
         x = np.ascontiguousarray(x, dtype=np.float64)
         (d / "in.bin").write_bytes(x.tobytes())
         subprocess.run([str(exe), str(d / "in.bin"), str(d / "out.bin")], check=True)
-        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 7)
+        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 9)
 
     return run
 
@@ -120,12 +123,29 @@ def test_angle_wrap_bit_identical_to_numpy(probe):
 
 def test_tilt_sincos_accuracy(probe):
     """sincos_tilt (no argument reduction) on the roll / pitch range of the
-    yaw-at-rest fast step: |a| <= pi/3 + 0.125."""
+    yaw-at-rest fast step: |a| <= pi/3 (every step starts inside the tilt clamp)."""
     rng = np.random.default_rng(3)
-    lim = np.pi / 3 + 0.125
+    lim = np.pi / 3
     a = np.concatenate([rng.uniform(-lim, lim, 300000), [0.0, -0.0, 1e-300, np.pi / 3, -np.pi / 3, lim, -lim]])
     out = probe(a)
     st, ct = out[:, 5], out[:, 6]
     assert np.max(ulp_err(st, np.sin(a))[np.abs(a) > 1e-300]) <= 1.0
     assert np.max(ulp_err(ct, np.cos(a))) <= 2.0  # as fast_sincos: the last step 1 + z*q rounds at ulp(1)/2
     assert st[300002] == 1e-300 and ct[300000] == 1.0 and st[300001] == 0.0
+
+
+def test_rate_sincos_accuracy(probe):
+    """rate_sincos: the stage offsets of the rate-bounded fast step,
+    |d| <= kRateAngle = 0.031 (dt * max commanded rate), and the rotation."""
+    rng = np.random.default_rng(4)
+    d = np.concatenate([rng.uniform(-0.031, 0.031, 200000), [0.0, -0.0, 1e-12, 0.031, -0.031]])
+    out = probe(d)
+    sr, cr = out[:, 7], out[:, 8]
+    assert np.max(ulp_err(sr, np.sin(d))[np.abs(d) > 1e-300]) <= 1.0
+    assert np.max(ulp_err(cr, np.cos(d))) <= 1.0
+    a = rng.uniform(-np.pi / 3, np.pi / 3, d.size)
+    base = probe(a)
+    s = base[:, 5] * cr + base[:, 6] * sr
+    c = base[:, 6] * cr - base[:, 5] * sr
+    assert np.max(np.abs(s - np.sin(a + d))) <= 4.5e-16
+    assert np.max(np.abs(c - np.cos(a + d))) <= 4.5e-16
