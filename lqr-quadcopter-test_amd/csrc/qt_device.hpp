@@ -78,6 +78,57 @@ struct Target {
   double p[3], v[3], a[3];
 };
 
+// Position / velocity / acceleration of a periodic pattern from the sin / cos
+// of its angles (circular target_motion.py:84-100, sinusoidal 142-153); the
+// caller has set o to the centre and zeros.
+template <bool WANT_ACC>
+__device__ __forceinline__ void periodic_state(const qt_env_params& e, int motion, const Pattern& pt,
+                                               const double* s, const double* c, Target& o) {
+  if (motion == QT_MOTION_CIRCULAR) {
+    const double r = e.radius, om = pt.c1;
+    o.p[0] = e.center[0] + r * c[0];
+    o.p[1] = e.center[1] + r * s[0];
+    o.v[0] = -r * om * s[0];
+    o.v[1] = r * om * c[0];
+    if (WANT_ACC) {
+      o.a[0] = -r * (om * om) * c[0];
+      o.a[1] = -r * (om * om) * s[0];
+    }
+  } else {
+    const double amp[3] = {e.amplitude, e.amplitude * 0.5, e.amplitude * 0.25};
+    const double om[3] = {pt.o0, pt.o1, pt.o2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      o.p[i] = e.center[i] + amp[i] * s[i];
+      o.v[i] = amp[i] * om[i] * c[i];
+      if (WANT_ACC) o.a[i] = -amp[i] * (om[i] * om[i]) * s[i];
+    }
+  }
+}
+
+// TargetMotion.get_state's acceleration clamp (target_motion.py:403-405).
+__device__ __forceinline__ void clamp_acceleration(const qt_env_params& e, Target& o) {
+  double am = norm3(o.a[0], o.a[1], o.a[2]);
+  if (am > e.max_acceleration) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o.a[i] = o.a[i] / am * e.max_acceleration;
+  }
+}
+
+// The periodic patterns' angles at time t: circular theta0 + omega t
+// (target_motion.py:84-86), sinusoidal 2 pi f_i t + phase_i (142-147).
+// Returns the number of angles (1 or 3).
+__device__ __forceinline__ int periodic_angles(int motion, const Pattern& pt, double t, double* th) {
+  if (motion == QT_MOTION_CIRCULAR) {
+    th[0] = pt.c0 + pt.c1 * t;
+    return 1;
+  }
+  th[0] = pt.o0 * t + pt.c0;
+  th[1] = pt.o1 * t + pt.c1;
+  th[2] = pt.o2 * t + pt.c2;
+  return 3;
+}
+
 // pattern.get_state(t) (target_motion.py:51-248) + TargetMotion.get_state's
 // acceleration clamp (403-405).  WANT_ACC = false skips the acceleration,
 // which only the feed-forward path reads (riccati_lqr.py:853-861).
@@ -96,31 +147,11 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     o.v[0] = pt.c0;
     o.v[1] = pt.c1;
     o.v[2] = pt.c2;
-  } else if (motion == QT_MOTION_CIRCULAR) {
-    double ang = pt.c0 + pt.c1 * t;
-    double s, c;
-    fast_sincos(ang, &s, &c);
-    const double r = e.radius, om = pt.c1;
-    o.p[0] = e.center[0] + r * c;
-    o.p[1] = e.center[1] + r * s;
-    o.v[0] = -r * om * s;
-    o.v[1] = r * om * c;
-    if (WANT_ACC) {
-      o.a[0] = -r * (om * om) * c;
-      o.a[1] = -r * (om * om) * s;
-    }
-  } else if (motion == QT_MOTION_SINUSOIDAL) {
-    const double amp[3] = {e.amplitude, e.amplitude * 0.5, e.amplitude * 0.25};
-    const double om[3] = {pt.o0, pt.o1, pt.o2};
-    const double ph[3] = {pt.c0, pt.c1, pt.c2};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      double s, c;
-      fast_sincos(om[i] * t + ph[i], &s, &c);
-      o.p[i] = e.center[i] + amp[i] * s;
-      o.v[i] = amp[i] * om[i] * c;
-      if (WANT_ACC) o.a[i] = -amp[i] * (om[i] * om[i]) * s;
-    }
+  } else if (motion == QT_MOTION_CIRCULAR || motion == QT_MOTION_SINUSOIDAL) {
+    double th[3], s[3], c[3];
+    const int na = periodic_angles(motion, pt, t, th);
+    for (int i = 0; i < na; ++i) fast_sincos(th[i], &s[i], &c[i]);
+    periodic_state<WANT_ACC>(e, motion, pt, s, c, o);
   } else if (motion == QT_MOTION_FIGURE8) {
     const double sc = e.amplitude, om = pt.o0;
     double st, ct;
@@ -146,13 +177,65 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
       o.a[2] = 0.0;
     }
   }
-  if (WANT_ACC) {
-    double am = norm3(o.a[0], o.a[1], o.a[2]);
-    if (am > e.max_acceleration) {
+  if (WANT_ACC) clamp_acceleration(e, o);
+}
+
+// Fast-step target of a periodic pattern (MOTION circular: one angle,
+// sinusoidal: three) with the sin / cos of its angles carried across steps.
+// Each step forms the angles exactly as target_state does (same expression,
+// same rounding) and rotates the carried sin / cos by the increment
+// d = theta_k - theta_{k-1} (~ omega dt: 0.041 rad for the default
+// sinusoid; small_sincos, |d| <= kSmallAngle) by angle addition, so they
+// follow sin / cos of the rounded angle the reference evaluates, with a drift
+// of a few ulp per step and none from t's accumulated rounding.  A wave with
+// an increment outside small_sincos's range takes fast_sincos for that step
+// (a uniform branch).
+template <int MOTION>
+struct PeriodicTrig {
+  static constexpr int NA = MOTION == QT_MOTION_SINUSOIDAL ? 3 : 1;
+  double th[NA], s[NA], c[NA];
+};
+
+template <int MOTION>
+__device__ __forceinline__ void periodic_trig_init(const Pattern& pt, double t, PeriodicTrig<MOTION>& r) {
+  double th[3];
+  periodic_angles(MOTION, pt, t, th);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) o.a[i] = o.a[i] / am * e.max_acceleration;
-    }
+  for (int i = 0; i < PeriodicTrig<MOTION>::NA; ++i) {
+    r.th[i] = th[i];
+    fast_sincos(th[i], &r.s[i], &r.c[i]);
   }
+}
+
+template <bool WANT_ACC, int MOTION>
+__device__ __forceinline__ void target_state_carried(const qt_env_params& e, const Pattern& pt, double t,
+                                                     PeriodicTrig<MOTION>& r, Target& o) {
+  constexpr int NA = PeriodicTrig<MOTION>::NA;
+  double th[3], d[NA], dm = 0.0;
+  periodic_angles(MOTION, pt, t, th);
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    d[i] = th[i] - r.th[i];
+    dm = fmax(dm, fabs(d[i]));
+    r.th[i] = th[i];
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(dm <= kSmallAngle)) == 0, 1)) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      double sd, cd;
+      small_sincos(d[i], &sd, &cd);
+      const double s0 = r.s[i], c0 = r.c[i];
+      r.s[i] = fma(s0, cd, c0 * sd);
+      r.c[i] = fma(c0, cd, -(s0 * sd));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) fast_sincos(th[i], &r.s[i], &r.c[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o.p[i] = e.center[i], o.v[i] = 0.0, o.a[i] = 0.0;
+  periodic_state<WANT_ACC>(e, MOTION, pt, r.s, r.c, o);
+  if (WANT_ACC) clamp_acceleration(e, o);
 }
 
 // ----------------------------------------------------------------- plant

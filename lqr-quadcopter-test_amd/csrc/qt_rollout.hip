@@ -183,6 +183,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
     se_pre = ep0 * ep0 + ep1 * ep1 + ep2 * ep2;
   }
+  // fast steps of a periodic pattern carry its angles' sin / cos (target_state_carried)
+  constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
+  PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
+  if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -223,7 +227,12 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       // the command is finite and inside the env clamps: parsing is the identity
       integrate<true, YAW0>(e, pl, x, u);
       t += e.dt;
-      if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
+      if (!(QT_ABLATE & QT_ABL_TARGET)) {
+        if constexpr (kCarry)
+          target_state_carried<FF, MOTION>(e, pt, t, ptrig, tg);
+        else
+          target_state<FF>(e, motion, pt, t, tg);
+      }
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
       se_pre = se;
