@@ -612,7 +612,8 @@ __host__ __device__ constexpr int structured_index(int j) {
 template <int KC, bool FF, bool KS, bool FAST = false>
 __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC, KS>& G, double hover,
                                                const double* qp, const double* qv, const Target& tg,
-                                               double* integ, double* u, double* diag = nullptr) {
+                                               double* integ, double* u, double* diag = nullptr,
+                                               double em_fast = 0.0) {
   double ep[3], ev[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 3; ++i) ep[i] = tg.p[i] - qp[i];
@@ -642,19 +643,26 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
   const double s[6] = {ep[0], ep[1], ep[2], ev[0], ev[1], ev[2]};
   double uf[4];
   if (KC == 9) {
-    double em = norm3(ep[0], ep[1], ep[2]);
+    // FAST: the caller passes ||e_p|| (the metric's pre-step error, the same
+    // correctly rounded square root of the same sum of squares), and the
+    // integral and errors are finite: sign(I) == sign(e) with |I| >= lim > 0
+    // (so I != 0) is "e has I's sign", and np.clip is fmin / fmax
+    const double em = FAST ? em_fast : norm3(ep[0], ep[1], ep[2]);
     const double lim = c.integral_limit;
     if (em > c.integral_zero_threshold) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        bool sat = fabs(integ[i]) >= lim && lim > 0;
-        bool worse = same_sign(integ[i], ep[i]);
-        if (!(sat && worse)) integ[i] += c.dt * ep[i];
+        bool block;
+        if (FAST)
+          block = (lim > 0) & (fabs(integ[i]) >= lim) & (integ[i] > 0 ? ep[i] > 0 : ep[i] < 0);
+        else
+          block = fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
+        if (!block) integ[i] += c.dt * ep[i];
       }
     }
     if (lim > 0) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i], -lim, lim);
+      for (int i = 0; i < 3; ++i) integ[i] = FAST ? clip_num(integ[i], -lim, lim) : clipd(integ[i], -lim, lim);
     }
     if (KS) {
       uf[0] = (G.k[0] * s[2] + G.k[1] * s[5]) + G.k[6] * integ[2];
@@ -727,7 +735,8 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
 template <bool FF, bool FAST = false>
 __device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, const double* g, double hover,
                                                    const double* qp, const double* qv, const Target& tg, double now,
-                                                   double* integ, double* u, double* diag = nullptr) {
+                                                   double* integ, double* u, double* diag = nullptr,
+                                               double em_fast = 0.0) {
   const double *kp = g, *ki = g + 3, *kd = g + 6;
   double ep[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
 #pragma unroll

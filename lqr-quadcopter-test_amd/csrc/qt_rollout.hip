@@ -191,19 +191,21 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
     double u[4];
+    // fast step: the pre-step tracking error, also the LQI's ||e_p|| (riccati_lqr.py:873)
+    const double err_fast = FAST ? sqrt_noscale(se_pre) : 0.0;
     if (QT_ABLATE & QT_ABL_CONTROLLER) {
       u[0] = hover, u[1] = u[2] = u[3] = 0.0;
     } else {
       if constexpr (KC == 3)
         compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
       else
-        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u);
+        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err_fast);
     }
     // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
     if (!(QT_ABLATE & QT_ABL_METRICS)) {
       double err, un;
       if (FAST) {
-        err = sqrt_noscale(se_pre);
+        err = err_fast;
         un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
       } else {
         const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
