@@ -187,6 +187,9 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
   if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
+  // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
+  Rk4Lin lin;
+  if constexpr (FAST && YAW0) lin = make_rk4_lin(e, pl);
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -227,7 +230,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     // ---- env.step (quadcopter_env.py:152-232)
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
-      integrate<true, YAW0>(e, pl, x, u);
+      if constexpr (YAW0)
+        integrate_yaw0(lin, pl, x, u);
+      else
+        integrate<true, false>(e, pl, x, u);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kCarry)
