@@ -399,11 +399,31 @@ __device__ __forceinline__ Rk4Lin make_rk4_lin(const qt_env_params& e, const Pla
   return L;
 }
 
+// Roll / pitch sin / cos carried across yaw-at-rest fast steps: the new
+// attitude differs from the step start's by |d| <= dt * max_rate (+ the
+// wrap's rounding; the tilt clamp only shortens it; rate_bounded_ok), so the
+// carried values are rotated by the exact difference of the rounded angles
+// with rate_sincos (angle addition): they follow sin / cos of the angles the
+// reference evaluates with a drift of a few ulp per step.
+__device__ __forceinline__ void attitude_trig_advance(const double* a_new, double* a_prev, Trig& ta) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    double sd, cd;
+    rate_sincos(a_new[i] - a_prev[i], &sd, &cd);
+    const double s0 = ta.s[i], c0 = ta.c[i];
+    ta.s[i] = fma(s0, cd, c0 * sd);
+    ta.c[i] = fma(c0, cd, -(s0 * sd));
+    a_prev[i] = a_new[i];
+  }
+}
+
 // One yaw-at-rest RK4 step in closed form (see Rk4Lin); x[8], x[11] untouched.
-__device__ __forceinline__ void integrate_yaw0(const Rk4Lin& L, const Plant& pl, double* x, const double* u) {
+// ta: sin / cos of roll and pitch at the step start (carried by the caller).
+__device__ __forceinline__ void integrate_yaw0(const Rk4Lin& L, const Plant& pl, const Trig& ta, double* x,
+                                               const double* u) {
   const double w0 = x[9], w1 = x[10];
   Trig t[4];
-  trig_of<true>(x + 6, t[0]);
+  t[0] = ta;
   const double d2[3] = {L.h2 * w0, L.h2 * w1, 0.0};
   const double d3[3] = {fma(L.d3y, w0, L.d3u * u[1]), fma(L.d3y, w1, L.d3u * u[2]), 0.0};
   const double d4[3] = {fma(L.d4y, w0, L.d4u * u[1]), fma(L.d4y, w1, L.d4u * u[2]), 0.0};
@@ -621,10 +641,12 @@ __host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ct
 // a = dt / 2 (10 + c), b = 5 dt; stages 3, 4 and the update likewise), so a
 // lane whose |w| starts within max_rate keeps every stage rate, and the next
 // step's rate, within max_rate (the rate clamp only shrinks it).  A stage
-// attitude offset h * w (h <= dt) is then at most dt * max_rate <= kRateAngle.
+// attitude offset h * w (h <= dt) is then at most dt * max_rate <= kRateAngle,
+// and with max_rate below max_angular_velocity the env's angular-velocity
+// clamp (quadcopter_env.py:446-450) never acts (constrain_fast_apply<true>).
 __host__ __device__ inline bool rate_bounded_ok(const qt_env_params& e, const qt_ctrl_params& c) {
   return c.max_rate >= 0.0 && e.drag_angular >= 0.0 && e.dt > 0.0 && e.dt * (10.0 + e.drag_angular) <= 1.0 &&
-         e.dt * c.max_rate * (1.0 + 1e-9) <= kRateAngle;
+         e.dt * c.max_rate * (1.0 + 1e-9) <= kRateAngle && c.max_rate * (1.0 + 1e-9) <= e.max_angular_velocity;
 }
 
 // Fast-path state constraints: the common case of _apply_state_constraints
@@ -652,8 +674,10 @@ __device__ __forceinline__ bool constrain_fast_ok(const qt_env_params& e, const 
 
 template <bool YAW0 = false>
 __device__ __forceinline__ void constrain_fast_apply(const qt_env_params& e, double* x) {
+  // YAW0 (rate-bounded, rate_bounded_ok): |w| <= max_rate < max_angular_velocity, the clip is inactive
+  if (!YAW0)
 #pragma unroll
-  for (int i = 9; i < (YAW0 ? 11 : 12); ++i) x[i] = clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+    for (int i = 9; i < 12; ++i) x[i] = clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
 #pragma unroll
   for (int i = 0; i < (YAW0 ? 2 : 3); ++i) {
     // (b % 2 pi) for b in (-2 pi, 4 pi): one correction, the same rounding as

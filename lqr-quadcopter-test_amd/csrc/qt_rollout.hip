@@ -188,8 +188,15 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
   if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
   // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
+  // and carried roll / pitch sin / cos (attitude_trig_advance)
   Rk4Lin lin;
-  if constexpr (FAST && YAW0) lin = make_rk4_lin(e, pl);
+  Trig ta;
+  double aprev[2];
+  if constexpr (FAST && YAW0) {
+    lin = make_rk4_lin(e, pl);
+    trig_of<true>(x + 6, ta);
+    aprev[0] = x[6], aprev[1] = x[7];
+  }
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -231,7 +238,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
       if constexpr (YAW0)
-        integrate_yaw0(lin, pl, x, u);
+        integrate_yaw0(lin, pl, ta, x, u);
       else
         integrate<true, false>(e, pl, x, u);
       t += e.dt;
@@ -252,9 +259,14 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       // if / else cost a taken branch around the else block every step.
       if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
+        if constexpr (YAW0) attitude_trig_advance(x + 6, aprev, ta);
         a.on_post += se < er2lo;
       } else {  // rare: exact constraints and comparison
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
+        if constexpr (YAW0) {  // restart the carried attitude trig (|roll|, |pitch| <= pi/3 again)
+          trig_of<true>(x + 6, ta);
+          aprev[0] = x[6], aprev[1] = x[7];
+        }
         a.on_post += norm_le(se, e.target_radius);
       }
       if (QT_ABLATE & QT_ABL_TERMINATION)
