@@ -345,23 +345,31 @@ __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant&
 // with acc_i = T R3(a_i) / m + g the stage's thrust + gravity acceleration.
 // The classic RK4 combination (_rk4_step, 295-317) of each linear part is
 // therefore a fixed linear map of (w, u) and of (v, acc_1..acc_4), whose
-// coefficients are the staged recurrences evaluated on unit inputs once per
-// lane (rk4_linear).  A step then costs about two operations per linear term
+// coefficients are the staged recurrences evaluated on unit inputs
+// (rk4_linear): once per launch on the host for the rates / attitudes
+// (make_rate_lin, a kernel argument) and once per lane for the velocities /
+// positions (make_vel_lin; per-episode mass).  A step then costs about two operations per linear term
 // instead of the stage-by-stage updates; the result equals the staged RK4 up
 // to the rounding of the reassociation (~1e-16 relative per step).
-struct Rk4Lin {
-  // w_new = wy w + wu u, a_new = a + ay w + au u, stage attitude offsets
-  // d2 = h2 w, d3 = d3y w + d3u u, d4 = d4y w + d4u u
+// Rates / attitudes (uniform: launch constants, computed on the host and
+// passed as a kernel argument, so they live in SGPRs):
+// w_new = wy w + wu u, a_new = a + ay w + au u, stage attitude offsets
+// d2 = h2 w, d3 = d3y w + d3u u, d4 = d4y w + d4u u.
+struct RateLin {
   double wy, wu, ay, au, h2, d3y, d3u, d4y, d4u;
-  // v_new = cv v + sum_i wv_i acc_i, p_new = p + pv v + sum_i pa_i acc_i
-  // (acc_4 does not reach the positions); gravity: gv = g sum wv, gp = g sum pa
+};
+
+// Velocities / positions (per lane: delta depends on the episode's mass):
+// v_new = cv v + sum_i wv_i acc_i, p_new = p + pv v + sum_i pa_i acc_i
+// (acc_4 does not reach the positions); gravity: gv = g sum wv, gp = g sum pa.
+struct VelLin {
   double cv, wv[4], pv, pa[3], gv, gp;
 };
 
 // Stage values of y' = f_i - lam y over one RK4 step of length h:
 // o = {y2, y3, y4, y_new, h/6 (y1 + 2 y2 + 2 y3 + y4)} (the last is the
 // step's integral of y, i.e. the update of a state whose derivative is y).
-__device__ __forceinline__ void rk4_linear(double lam, double h, double y, const double* f, double* o) {
+QT_HD void rk4_linear(double lam, double h, double y, const double* f, double* o) {
   const double k1 = f[0] - lam * y, y2 = y + 0.5 * h * k1;
   const double k2 = f[1] - lam * y2, y3 = y + 0.5 * h * k2;
   const double k3 = f[2] - lam * y3, y4 = y + h * k3;
@@ -371,9 +379,9 @@ __device__ __forceinline__ void rk4_linear(double lam, double h, double y, const
   o[4] = h / 6.0 * (y + 2.0 * y2 + 2.0 * y3 + y4);
 }
 
-__device__ __forceinline__ Rk4Lin make_rk4_lin(const qt_env_params& e, const Plant& pl) {
-  Rk4Lin L;
-  const double h = e.dt, lam = 10.0 + e.drag_angular, delta = e.drag_linear * pl.inv_mass;
+QT_HD RateLin make_rate_lin(const qt_env_params& e) {
+  RateLin L;
+  const double h = e.dt, lam = 10.0 + e.drag_angular;
   const double zero[4] = {0.0, 0.0, 0.0, 0.0}, ten[4] = {10.0, 10.0, 10.0, 10.0};
   double o[5];
   rk4_linear(lam, h, 1.0, zero, o);
@@ -381,6 +389,14 @@ __device__ __forceinline__ Rk4Lin make_rk4_lin(const qt_env_params& e, const Pla
   rk4_linear(lam, h, 0.0, ten, o);
   L.wu = o[3], L.au = o[4], L.d3u = 0.5 * h * o[0], L.d4u = h * o[1];
   L.h2 = 0.5 * h;
+  return L;
+}
+
+__device__ __forceinline__ VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
+  VelLin L;
+  const double h = e.dt, delta = e.drag_linear * pl.inv_mass;
+  const double zero[4] = {0.0, 0.0, 0.0, 0.0};
+  double o[5];
   rk4_linear(delta, h, 1.0, zero, o);
   L.cv = o[3], L.pv = o[4];
   double sw = 0.0, sp = 0.0;
@@ -417,16 +433,16 @@ __device__ __forceinline__ void attitude_trig_advance(const double* a_new, doubl
   }
 }
 
-// One yaw-at-rest RK4 step in closed form (see Rk4Lin); x[8], x[11] untouched.
+// One yaw-at-rest RK4 step in closed form (RateLin, VelLin); x[8], x[11] untouched.
 // ta: sin / cos of roll and pitch at the step start (carried by the caller).
-__device__ __forceinline__ void integrate_yaw0(const Rk4Lin& L, const Plant& pl, const Trig& ta, double* x,
-                                               const double* u) {
+__device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L, const Plant& pl, const Trig& ta,
+                                               double* x, const double* u) {
   const double w0 = x[9], w1 = x[10];
   Trig t[4];
   t[0] = ta;
-  const double d2[3] = {L.h2 * w0, L.h2 * w1, 0.0};
-  const double d3[3] = {fma(L.d3y, w0, L.d3u * u[1]), fma(L.d3y, w1, L.d3u * u[2]), 0.0};
-  const double d4[3] = {fma(L.d4y, w0, L.d4u * u[1]), fma(L.d4y, w1, L.d4u * u[2]), 0.0};
+  const double d2[3] = {R.h2 * w0, R.h2 * w1, 0.0};
+  const double d3[3] = {fma(R.d3y, w0, R.d3u * u[1]), fma(R.d3y, w1, R.d3u * u[2]), 0.0};
+  const double d4[3] = {fma(R.d4y, w0, R.d4u * u[1]), fma(R.d4y, w1, R.d4u * u[2]), 0.0};
   trig_shift<true, true>(x + 6, t[0], d2, t[1]);
   trig_shift<true, true>(x + 6, t[0], d3, t[2]);
   trig_shift<true, true>(x + 6, t[0], d4, t[3]);
@@ -451,10 +467,10 @@ __device__ __forceinline__ void integrate_yaw0(const Rk4Lin& L, const Plant& pl,
     x[j] = fma(tm, sp[j], fma(L.pv, v, j == 2 ? x[j] + L.gp : x[j]));
     x[3 + j] = fma(tm, sv[j], j == 2 ? fma(L.cv, v, L.gv) : L.cv * v);
   }
-  x[6] = fma(L.ay, w0, fma(L.au, u[1], x[6]));
-  x[7] = fma(L.ay, w1, fma(L.au, u[2], x[7]));
-  x[9] = fma(L.wy, w0, L.wu * u[1]);
-  x[10] = fma(L.wy, w1, L.wu * u[2]);
+  x[6] = fma(R.ay, w0, fma(R.au, u[1], x[6]));
+  x[7] = fma(R.ay, w1, fma(R.au, u[2], x[7]));
+  x[9] = fma(R.wy, w0, R.wu * u[1]);
+  x[10] = fma(R.wy, w1, R.wu * u[2]);
 }
 
 // _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held

@@ -172,7 +172,8 @@ template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
 __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
                                           const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
-                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep) {
+                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep,
+                                          const RateLin& rl) {
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
@@ -189,11 +190,11 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
   // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
   // and carried roll / pitch sin / cos (attitude_trig_advance)
-  Rk4Lin lin;
+  VelLin lin;
   Trig ta;
   double aprev[2];
   if constexpr (FAST && YAW0) {
-    lin = make_rk4_lin(e, pl);
+    lin = make_vel_lin(e, pl);
     trig_of<true>(x + 6, ta);
     aprev[0] = x[6], aprev[1] = x[7];
   }
@@ -238,7 +239,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
       if constexpr (YAW0)
-        integrate_yaw0(lin, pl, ta, x, u);
+        integrate_yaw0(rl, lin, pl, ta, x, u);
       else
         integrate<true, false>(e, pl, x, u);
       t += e.dt;
@@ -312,7 +313,7 @@ constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
-                                                         double* __restrict__ rec, int deferred) {
+                                                         double* __restrict__ rec, int deferred, RateLin rl) {
   const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (slot >= b.slot_end) return;
   const int64_t n = b.n, ep = episode_of(b, slot);
@@ -360,11 +361,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   if (FLAVOR != kExact) {
     if (!wave_ok) return;
     run_steps<true, FLAVOR == kYaw0, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a,
-                                                         nsteps, rec, n, ep);
+                                                         nsteps, rec, n, ep, rl);
   } else {
     if (deferred != kExact && wave_ok) return;
     run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
-                                                n, ep);
+                                                n, ep, rl);
   }
 
 #pragma unroll
@@ -717,14 +718,15 @@ int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH
 template <int MOTION, int KC, bool FF, bool KS>
 void launch_flavours(bool fast, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                      const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
+  const RateLin rl = make_rate_lin(e);  // yaw-at-rest closed-form RK4 (integrate_yaw0)
   if (fast && KS && rate_bounded_ok(e, c)) {
-    rollout_kernel<kYaw0, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kYaw0);
+    rollout_kernel<kYaw0, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kYaw0, rl);
   } else if (fast) {
-    rollout_kernel<kFast, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kFast);
+    rollout_kernel<kFast, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kFast, rl);
   } else {
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact);
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
   }
 }
 
