@@ -787,18 +787,17 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
   if (KC == 9) {
     // FAST: the caller passes ||e_p|| (the metric's pre-step error, the same
     // correctly rounded square root of the same sum of squares), and the
-    // integral and errors are finite: sign(I) == sign(e) with |I| >= lim > 0
-    // (so I != 0) is "e has I's sign", and np.clip is fmin / fmax
+    // integral and errors are finite.  The anti-windup block then needs no
+    // test: it holds only when lim > 0, |I| >= lim and e has I's sign, and
+    // then |I + dt e| >= |I| >= lim (rounding is monotone), so the clip below
+    // returns sign(I) lim — which is I when |I| == lim, and what the
+    // reference's clip makes of a blocked |I| > lim.  np.clip is fmin / fmax.
     const double em = FAST ? em_fast : norm3(ep[0], ep[1], ep[2]);
     const double lim = c.integral_limit;
     if (em > c.integral_zero_threshold) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        bool block;
-        if (FAST)
-          block = (lim > 0) & (fabs(integ[i]) >= lim) & (integ[i] > 0 ? ep[i] > 0 : ep[i] < 0);
-        else
-          block = fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
+        const bool block = !FAST && fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
         if (!block) integ[i] += c.dt * ep[i];
       }
     }
