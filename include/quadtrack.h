@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 1
+#define QT_ABI_VERSION 2
 
 /* error codes */
 #define QT_OK 0
@@ -152,7 +152,10 @@ typedef struct qt_batch {
   int32_t k_structured;         /* 1: the caller asserts every K entry outside the per-axis
                                    pattern (z->thrust, y->roll, x->pitch) is exactly 0, as the
                                    diagonal-weight DARE produces; the kernel then skips them */
-  int32_t pad_;
+  int32_t k_no_yaw;             /* 1: the caller asserts the yaw-rate row of K is exactly 0 (B has
+                                   no yaw column, riccati_lqr.py:215-232, so any DARE gain has
+                                   it): yaw never moves from rest and the yaw-at-rest fast
+                                   flavour applies to dense gains too */
   const int32_t* order;         /* [n] or NULL */
 } qt_batch;
 

@@ -351,7 +351,8 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
                   all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && isfinite(hover) &&
                   isfinite(pl.inv_mass) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
-  // structured gains never command yaw: a yaw at rest stays exactly zero
+  // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
+  // never command yaw: a yaw at rest stays exactly zero
   // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
   // rate-bounded, roll and pitch rates within the command clip: rate_bounded_ok)
   if (FLAVOR == kYaw0 || deferred == kYaw0)
@@ -716,10 +717,10 @@ int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
 int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
 
 template <int MOTION, int KC, bool FF, bool KS>
-void launch_flavours(bool fast, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+void launch_flavours(bool fast, bool no_yaw, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                      const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
   const RateLin rl = make_rate_lin(e);  // yaw-at-rest closed-form RK4 (integrate_yaw0)
-  if (fast && KS && rate_bounded_ok(e, c)) {
+  if (fast && (KS || no_yaw) && rate_bounded_ok(e, c)) {
     rollout_kernel<kYaw0, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
     rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kYaw0, rl);
   } else if (fast) {
@@ -731,50 +732,50 @@ void launch_flavours(bool fast, int grid, hipStream_t s, const qt_env_params& e,
 }
 
 template <int KC, bool FF, bool KS>
-void launch_rollout_motion(int motion, bool fast, int grid, hipStream_t s, const qt_env_params& e,
+void launch_rollout_motion(int motion, bool fast, bool no_yaw, int grid, hipStream_t s, const qt_env_params& e,
                            const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st,
                            int nsteps, double* rec) {
   switch (motion) {
     case QT_MOTION_STATIONARY:
-      launch_flavours<QT_MOTION_STATIONARY, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_STATIONARY, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_LINEAR:
-      launch_flavours<QT_MOTION_LINEAR, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_LINEAR, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_CIRCULAR:
-      launch_flavours<QT_MOTION_CIRCULAR, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_CIRCULAR, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_SINUSOIDAL:
-      launch_flavours<QT_MOTION_SINUSOIDAL, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_SINUSOIDAL, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     case QT_MOTION_FIGURE8:
-      launch_flavours<QT_MOTION_FIGURE8, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<QT_MOTION_FIGURE8, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
       break;
     default:
-      launch_flavours<-1, KC, FF, KS>(fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_flavours<-1, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
   }
 }
 
 template <int KC>
-void launch_rollout(bool ff, bool ks, int motion, int grid, hipStream_t s, const qt_env_params& e,
+void launch_rollout(bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                     const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                     double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
   if constexpr (KC == 3) {  // PID never commands yaw (controllers/__init__.py:373): the yaw-at-rest flavour applies
     if (ff)
-      launch_rollout_motion<3, true, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<3, true, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
     else
-      launch_rollout_motion<3, false, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<3, false, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
   } else if (ff) {
     if (ks)
-      launch_rollout_motion<KC, true, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, true, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
     else
-      launch_rollout_motion<KC, true, false>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, true, false>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
   } else {
     if (ks)
-      launch_rollout_motion<KC, false, true>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, false, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
     else
-      launch_rollout_motion<KC, false, false>(motion, fast, grid, s, e, c, cr, b, st, nsteps, rec);
+      launch_rollout_motion<KC, false, false>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
   }
 }
 
@@ -808,12 +809,13 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   hipStream_t s = (hipStream_t)stream;
   const bool ff = ctrl->feedforward_enabled != 0;
   const bool ks = batch->k_structured != 0;
+  const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
   if (batch->k_cols == 9)
-    launch_rollout<9>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    launch_rollout<9>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   else if (batch->k_cols == 3)
-    launch_rollout<3>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    launch_rollout<3>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   else
-    launch_rollout<6>(ff, ks, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+    launch_rollout<6>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
   return check_launch();
 }
 
@@ -835,17 +837,18 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
   hipStream_t s = (hipStream_t)stream;
   const bool ff = ctrl->feedforward_enabled != 0;
   const bool ks = batch->k_structured != 0;
+  const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
   for (int32_t i = 0; i < nseg; ++i) {
     b.slot0 = i ? seg_end[i - 1] : 0;
     b.slot_end = seg_end[i];
     if (b.slot_end == b.slot0) continue;
     const int grid = grid_of(b.slot_end - b.slot0);
     if (batch->k_cols == 9)
-      launch_rollout<9>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+      launch_rollout<9>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
     else if (batch->k_cols == 3)
-      launch_rollout<3>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+      launch_rollout<3>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
     else
-      launch_rollout<6>(ff, ks, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+      launch_rollout<6>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
   }
   return QT_OK;

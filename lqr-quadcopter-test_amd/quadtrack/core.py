@@ -40,6 +40,7 @@ class EpisodeBatch:
     hover: torch.Tensor | None = None         # [n]
     order: torch.Tensor | None = None         # [n] int32
     k_structured: bool = False                # every off-axis K entry is exactly zero
+    k_no_yaw: bool = False                    # the yaw-rate row of K is exactly zero
     groups: tuple | None = None               # (seg_motion, seg_end): `order` groups slots by motion
 
     def c_batch(self, with_k=True) -> Batch:
@@ -53,6 +54,7 @@ class EpisodeBatch:
         b.k_cols = self.k_cols
         b.k_per_episode = int(self.K.shape[1] != 1)
         b.k_structured = int(self.k_structured)
+        b.k_no_yaw = int(self.k_no_yaw)
         b.order = ptr(self.order)
         return b
 
@@ -64,7 +66,8 @@ class EpisodeBatch:
         K = self.K if self.K.shape[1] == 1 else col(self.K)
         return EpisodeBatch(n=idx.numel(), device=self.device, pattern=col(self.pattern), offset=col(self.offset), K=K,
                             k_cols=self.k_cols, motion=col(self.motion), plant_mass=col(self.plant_mass),
-                            hover=col(self.hover), k_structured=self.k_structured)
+                            hover=col(self.hover), k_structured=self.k_structured,
+                            k_no_yaw=self.k_no_yaw)
 
 
 @dataclass
@@ -110,6 +113,15 @@ def gains_structured(K: torch.Tensor, k_cols: int) -> bool:
     for r, c in _AXIS_PATTERN[k_cols]:
         mask[r * k_cols + c] = False
     return bool((K[mask] == 0).all().item())
+
+
+def gains_no_yaw(K: torch.Tensor, k_cols: int) -> bool:
+    """True when the yaw-rate row of K ([4*k_cols, m], row 3) is exactly zero
+    (qt_batch.k_no_yaw): the DARE gains always (B has no yaw column), the
+    heuristic LQR always (controllers/__init__.py:560-574), PID by design."""
+    if k_cols == 3:
+        return True
+    return bool((K[3 * k_cols:4 * k_cols] == 0).all().item())
 
 
 def to_device(a, device, dtype=F64) -> torch.Tensor:

@@ -247,7 +247,8 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
     od = None if order is None else torch.as_tensor(np.asarray(order, dtype=np.int32), device=dev)
     b = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pat, dev), offset=core.to_device(off, dev),
                           K=controller.K, k_cols=controller.k_cols, motion=mo, plant_mass=pm, hover=controller.hover,
-                          order=od, k_structured=controller.k_structured, groups=groups)
+                          order=od, k_structured=controller.k_structured,
+                          k_no_yaw=core.gains_no_yaw(controller.K, controller.k_cols), groups=groups)
     return b
 
 

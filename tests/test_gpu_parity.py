@@ -220,6 +220,40 @@ def test_periodic_target_carried_trig(qt, cfg):
     assert np.isfinite(tg).all()
 
 
+@pytest.mark.parametrize("lqi", [False, True])
+def test_dense_gains_yaw_at_rest(qt, lqi):
+    """A full (coupled) Q gives a dense K, whose yaw-rate row is still exactly
+    zero (B has no yaw column): the batch asserts k_no_yaw and takes the
+    yaw-at-rest fast flavour with dense gains.  Against the oracle's DARE +
+    rollout, and against the exact step (recording)."""
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    Q = np.diag([1e-4, 1e-4, 16.0, 0.0036, 0.0036, 4.0])
+    Q[0, 1] = Q[1, 0] = 5e-5
+    Q[0, 3] = Q[3, 0] = 2e-4
+    Q[2, 5] = Q[5, 2] = 0.5
+    ctl_cfg = {"dt": 0.01, "Q": Q.tolist()}
+    if lqi:
+        ctl_cfg.update(use_lqi=True, q_int=[1e-3, 1e-3, 1e-2])
+    env_cfg = {"target": {"motion_type": "circular"}}
+    ctl = BatchedRiccatiLQR(ctl_cfg)
+    assert not ctl.k_structured and core.gains_no_yaw(ctl.K, ctl.k_cols)
+    n = 512
+    seeds = np.arange(n)
+    fast = run_closed_loop(ctl, env_cfg, n=n, seeds=seeds)
+    exact = run_closed_loop(ctl, env_cfg, n=n, seeds=seeds, record=True)
+    np.testing.assert_allclose(fast.metrics.cpu().numpy(), exact.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    env = O.env_params(env_cfg)
+    c, K, kc, _, _ = O.controller(ctl_cfg)
+    pat, off = O.draws("circular", seeds)
+    x0 = np.array([O.initial_state(env, env.motion, pat[i], off[i]) for i in range(n)]).reshape(-1, 12)
+    om, oxf, _, _ = O.rollout(env, c, O.criteria(), None, pat.reshape(-1, 4), None, None, K, kc, False, x0)
+    np.testing.assert_allclose(fast.metrics.cpu().numpy().T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=TOL)
+
+
 @pytest.mark.parametrize("motion", ["stationary", "circular"])
 def test_carried_trig_long_horizon(qt, motion):
     """Ten times the default horizon (300 s, 30,000 steps) vs the oracle: the
