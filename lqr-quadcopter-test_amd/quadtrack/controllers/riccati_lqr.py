@@ -449,9 +449,9 @@ class BatchedRiccatiLQR:
         # riccati_lqr.py:568-577, 637-641), unless per-episode arrays are given
         if Q is None and config.get("Q") is not None:
             Qs = _build_Q(config, self.use_lqi, qi).astype(float)
-            Q = np.broadcast_to(Qs, (m,) + Qs.shape)
+            Q = np.broadcast_to(Qs, (m,) + Qs.shape).copy()
         if R is None and config.get("R") is not None:
-            R = np.broadcast_to(_build_R(config).astype(float), (m, 4, 4))
+            R = np.broadcast_to(_build_R(config).astype(float), (m, 4, 4)).copy()
         if Q is None:
             Qd = np.empty((m, self.n_state))
             Qd[:, 0:3] = np.broadcast_to(np.asarray(q_pos if q_pos is not None else config.get("q_pos", [1e-4, 1e-4, 16.0]), float), (m, 3))
