@@ -132,7 +132,11 @@ __device__ __forceinline__ int periodic_angles(int motion, const Pattern& pt, do
 // pattern.get_state(t) (target_motion.py:51-248) + TargetMotion.get_state's
 // acceleration clamp (403-405).  WANT_ACC = false skips the acceleration,
 // which only the feed-forward path reads (riccati_lqr.py:853-861).
-template <bool WANT_ACC>
+// RECIP (fast step, no acceleration wanted): the figure-8's four divisions
+// by den and den^2 become one correctly rounded reciprocal and products
+// (<= 2 ulp per component; without feed-forward no forward difference reads
+// them).
+template <bool WANT_ACC, bool RECIP = false>
 __device__ __forceinline__ void target_state(const qt_env_params& e, int motion, const Pattern& pt, double t,
                                              Target& o) {
   o.p[0] = e.center[0];
@@ -157,13 +161,21 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     double st, ct;
     fast_sincos(om * t, &st, &ct);
     double den = 1.0 + st * st;
-    o.p[0] = e.center[0] + sc * ct / den;
-    o.p[1] = e.center[1] + sc * st * ct / den;
     double dcos = -st * om, dsin = ct * om;
     double dden = 2.0 * st * dsin;
     double den2 = den * den;
-    o.v[0] = sc * ((dcos * den - ct * dden) / den2);
-    o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
+    if (RECIP && !WANT_ACC) {
+      const double r = 1.0 / den, r2 = r * r;
+      o.p[0] = e.center[0] + sc * ct * r;
+      o.p[1] = e.center[1] + sc * st * ct * r;
+      o.v[0] = sc * ((dcos * den - ct * dden) * r2);
+      o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) * r2);
+    } else {
+      o.p[0] = e.center[0] + sc * ct / den;
+      o.p[1] = e.center[1] + sc * st * ct / den;
+      o.v[0] = sc * ((dcos * den - ct * dden) / den2);
+      o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
+    }
     if (WANT_ACC) {
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;

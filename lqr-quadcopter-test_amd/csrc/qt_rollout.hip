@@ -247,7 +247,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
         if constexpr (kCarry)
           target_state_carried<FF, MOTION>(e, pt, t, ptrig, tg);
         else
-          target_state<FF>(e, motion, pt, t, tg);
+          target_state<FF, true>(e, motion, pt, t, tg);
       }
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
