@@ -806,10 +806,16 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
     // reference's clip makes of a blocked |I| > lim.  np.clip is fmin / fmax.
     const double em = FAST ? em_fast : norm3(ep[0], ep[1], ep[2]);
     const double lim = c.integral_limit;
-    if (em > c.integral_zero_threshold) {
+    if (FAST) {
+      // the threshold gate as a step size: I + 0 e == I (up to the sign of a
+      // zero integral, which no later operation distinguishes)
+      const double g = em > c.integral_zero_threshold ? c.dt : 0.0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) integ[i] = fma(g, ep[i], integ[i]);
+    } else if (em > c.integral_zero_threshold) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const bool block = !FAST && fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
+        const bool block = fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
         if (!block) integ[i] += c.dt * ep[i];
       }
     }
