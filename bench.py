@@ -14,7 +14,11 @@ all-reduce of the metric vector when N > 1).  value = all ranks' env-steps /
 max-over-ranks wall time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-(N > 1 is launched by torch.distributed.run, one process per GPU.)
+N > 1 runs one process per GPU under torch.distributed.run: when WORLD_SIZE is
+unset, bench.py starts `python -m torch.distributed.run --nproc-per-node N`
+on itself as a child process (before any GPU call) and exits with its code;
+under a launcher, --gpus must equal WORLD_SIZE.  --gpus N with fewer than N
+visible GPUs is an error, never a silent 1-GPU run.
 """
 
 from __future__ import annotations
@@ -37,6 +41,8 @@ sys.path.insert(0, os.path.join(ROOT, "lqr-quadcopter-test_amd"))
 FLOPS_PER_ENV_STEP = 429
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, spec (half the FP32 vector 157.3 TF/s)
 HBM_PEAK_GBS = 8000.0
+# the dominant kernel of the bench workload: yaw-at-rest fast flavour, linear target, 6-column structured K
+KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true>"
 
 
 def parse():
@@ -47,19 +53,77 @@ def parse():
     ap.add_argument("--episodes", type=int, default=65536, help="episodes per GPU")
     ap.add_argument("--motion", default="linear")
     ap.add_argument("--cpu-sample", type=int, default=65536, help="episodes in the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--cpu-sample-1core", type=int, default=4096, help="episodes of the 1-thread CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU plumbing check of the N-rank launch (gloo, no kernels): prints the ranks seen")
     return ap.parse_args()
+
+
+def launch(args) -> int:
+    """Re-run this script as N ranks under torch.distributed.run (child
+    process, no exec; nothing here has touched the GPU)."""
+    import socket
+    import subprocess
+
+    if not args.launcher_check:
+        import torch
+
+        visible = torch.cuda.device_count()  # a count, not a GPU initialisation
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) are visible", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_check(world: int, rank: int):
+    """The ranks' view of the launch, on CPU (gloo): rank 0 prints one line."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    seen = dist.get_world_size() if world > 1 else 1
+    ranks = torch.tensor([rank], dtype=torch.int64)
+    if world > 1:
+        out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(out, ranks)
+        ranks_all = [int(t.item()) for t in out]
+    else:
+        ranks_all = [0]
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "n_gpus": world, "world_size_seen": seen, "ranks": ranks_all}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.launcher_check:
+        return launcher_check(world, rank)
+    import torch
+    import torch.distributed as dist
+
+    if torch.cuda.device_count() <= local:
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -125,7 +189,13 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     steps_done = met[core._abi.MET["steps"]].sum()
     local_env_steps = float(steps_done.item())  # this rank's executed env-steps per pass
+    per_rank = [local_env_steps]
+    seen = 1
     if world > 1:
+        seen = dist.get_world_size()  # the ranks RCCL saw
+        gathered = [torch.zeros_like(steps_done) for _ in range(world)]
+        dist.all_gather(gathered, steps_done)
+        per_rank = [float(v.item()) for v in gathered]
         dist.all_reduce(steps_done)
     env_steps_per_pass = float(steps_done.item())  # all ranks, executed steps of the last pass
     value = env_steps_per_pass * args.steps / elapsed
@@ -164,10 +234,20 @@ def main():
     if rank == 0:
         achieved = FLOPS_PER_ENV_STEP * local_env_steps / (kern_ms * 1e-3) / 1e12
         # the dominant kernel: the fast yaw-at-rest flavour (older profiles: the single-flavour kernel)
-        traffic, traffic_src = pmc_traffic(("rollout_kernel<2, 1, 6, false, true>", "rollout_kernel<1, 6, false, true>"))
+        traffic, traffic_src = pmc_traffic((KERNEL_TAG,))
         # algorithmic HBM bytes of one launch: per-episode state in (x 12, target 9, t, acc 14,
         # pattern 3 doubles) and out (x, target, t, acc); gains are a broadcast
         algo_bytes = (39 + 36) * 8 * n
+        # the same frac from the committed rocprofv3 kernel trace (fast launch alone; its deferred
+        # exact pass runs no wave at this workload)
+        prof = profiled_kernel((KERNEL_TAG,))
+        prof_line = None
+        if prof is not None:
+            p_ms, p_min, p_calls, p_dir = prof
+            p_ach = FLOPS_PER_ENV_STEP * local_env_steps / (p_ms * 1e-3) / 1e12
+            prof_line = {"source": f"{p_dir}/kernel_stats.csv", "kernel_avg_ms": round(p_ms, 4),
+                         "kernel_min_ms": round(p_min, 4), "calls": p_calls, "achieved": round(p_ach, 3),
+                         "frac": round(p_ach / FP64_PEAK_TFLOPS, 4)}
         line = {
             "metric": "env-steps/sec at 65 536 parallel episodes per GPU (30 s @ dt=0.01, Riccati-LQR closed loop)",
             "value": round(value, 1),
@@ -193,7 +273,10 @@ def main():
                          "kernel": "rollout_kernel<yaw-at-rest fast step, LINEAR, K=6, no-FF, structured K> "
                                    "+ its deferred exact pass (HIP events around both)",
                          "kernel_ms": round(kern_ms, 4),
-                         "flops_per_env_step": FLOPS_PER_ENV_STEP},
+                         "flops_per_env_step": FLOPS_PER_ENV_STEP,
+                         "profiled": prof_line},
+            "ranks": {"world_size_seen": seen, "backend": "nccl (RCCL)" if world > 1 else None,
+                      "env_steps_per_pass_per_rank": per_rank},
             "cpu_baseline": cpu,
             "tracking": track,
             "dare": dare,
@@ -201,6 +284,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def profiled_kernel(kernel_tags):
+    """Average duration (ms) of the dominant kernel in the newest committed
+    rocprofv3 kernel trace (profiles/r*/kernel_stats.csv) whose kernel name
+    contains one of `kernel_tags`: (avg_ms, min_ms, calls, profile dir)."""
+    import csv
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats.csv")), reverse=True):
+        for tag in kernel_tags:
+            rows = [r for r in csv.DictReader(open(path)) if tag in r["Name"]]
+            if rows:
+                r = rows[0]
+                return (float(r["AverageNs"]) * 1e-6, float(r["MinNs"]) * 1e-6, int(r["Calls"]),
+                        os.path.relpath(os.path.dirname(path), ROOT))
+    return None
 
 
 def pmc_traffic(kernel_tags):
@@ -231,8 +331,10 @@ def pmc_traffic(kernel_tags):
 
 def cpu_baseline(args, cfg, seeds, gpu_met):
     """The oracle (C restatement of the reference loop, oracle/) on the host
-    cores over a bounded sample of the same episodes; also returns the max
-    |GPU - oracle| over that sample's per-episode metrics."""
+    cores over bounded samples of the same episodes: one core on the first
+    --cpu-sample-1core episodes, then OpenMP over the host threads on the
+    first --cpu-sample; also returns the max |GPU - oracle| over the latter's
+    per-episode metrics."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -240,16 +342,25 @@ def cpu_baseline(args, cfg, seeds, gpu_met):
     c, K, kc, _, _ = O.controller({"dt": 0.01})
     pat, off = O.draws(args.motion, seeds)
     x0 = np.array([O.initial_state(env, env.motion, pat[i], off[i]) for i in range(len(seeds))])
-    t0 = time.perf_counter()
-    met, xf, _, threads = O.rollout(env, c, O.criteria(), None, pat, None, None, K, kc, False, x0,
-                                    threads=args.cpu_threads or None)
-    dt = time.perf_counter() - t0
+
+    def timed(m, threads):
+        t0 = time.perf_counter()
+        met, _, _, used = O.rollout(env, c, O.criteria(), None, pat[:m], None, None, K, kc, False, x0[:m],
+                                    threads=threads)
+        return met, time.perf_counter() - t0, used
+
+    m1 = min(args.cpu_sample_1core, len(seeds))
+    met1, dt1, _ = timed(m1, 1)
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    met, dt, used = timed(len(seeds), threads)
     steps = float(met[:, -1].sum())
     diff = float(np.max(np.abs(gpu_met.cpu().numpy().T - met)))
-    cpu = {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": int(threads), "kind": "port",
+    cpu = {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": int(used), "kind": "port",
            "sample": f"{len(seeds)} episodes x 3000 steps of the same workload (oracle/qt_oracle.c, FP64, "
-                     f"OpenMP over episodes), {dt:.2f} s wall",
-           "cpu_model": _cpu_model()}
+                     f"OpenMP over episodes, {int(used)} threads), {dt:.2f} s wall",
+           "single_core": {"value": round(float(met1[:, -1].sum()) / dt1, 1), "cores": 1,
+                           "sample": f"first {m1} episodes x 3000 steps, 1 thread, {dt1:.2f} s wall"},
+           "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
     return cpu, diff
 
 

@@ -23,6 +23,19 @@ using namespace qt;
 #define QT_ABL_CONTROLLER 8
 #define QT_ABL_TARGET 16
 
+// Diagnostic clock-stamp build (scripts/clock_stamp.py; -DQT_CLOCK_STAMP=1):
+// lane 0 of every wave of a fast-flavour launch records s_memtime (shader
+// clock) and s_memrealtime (100 MHz) around its step loop into a buffer of
+// its own, which no other code reads; qt_debug_stamps copies it out.  The
+// product build has QT_CLOCK_STAMP == 0 and executes no stamp.
+#ifndef QT_CLOCK_STAMP
+#define QT_CLOCK_STAMP 0
+#endif
+#if QT_CLOCK_STAMP
+constexpr int kStampWaves = 1 << 16;
+__device__ unsigned long long g_qt_stamps[kStampWaves][4];
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -361,8 +374,19 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
   if (FLAVOR != kExact) {
     if (!wave_ok) return;
+#if QT_CLOCK_STAMP
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     run_steps<true, FLAVOR == kYaw0, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a,
                                                          nsteps, rec, n, ep, rl);
+#if QT_CLOCK_STAMP
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    const int64_t wave = (slot - b.slot0) >> 6;
+    if ((threadIdx.x & 63) == 0 && wave < kStampWaves) {
+      g_qt_stamps[wave][0] = t0, g_qt_stamps[wave][1] = t1;
+      g_qt_stamps[wave][2] = r0, g_qt_stamps[wave][3] = r1;
+    }
+#endif
   } else {
     if (deferred != kExact && wave_ok) return;
     run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
@@ -788,6 +812,17 @@ bool valid_state(const qt_state& st, bool need_integ) {
 extern "C" {
 
 int qt_abi_version(void) { return QT_ABI_VERSION; }
+
+#if QT_CLOCK_STAMP
+// Diagnostic build only: copy the first `waves` stamp records
+// {memtime start, end, realtime start, end} to host memory out[waves][4].
+int qt_debug_stamps(unsigned long long* out, int64_t waves) {
+  if (!out || waves < 0 || waves > kStampWaves) return QT_EINVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 4 * waves) == hipSuccess
+             ? QT_OK
+             : QT_ELAUNCH;
+}
+#endif
 
 int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, qt_state st, void* stream) {
   if (!env || !batch || batch->n < 0) return QT_EINVAL;
