@@ -129,6 +129,25 @@ __device__ __forceinline__ int periodic_angles(int motion, const Pattern& pt, do
   return 3;
 }
 
+// Figure-8 position / velocity (target_motion.py:173-204) from sin / cos of
+// theta = omega t, without the acceleration: the four divisions by den and
+// den^2 as one correctly rounded reciprocal and products (<= 2 ulp per
+// component; without feed-forward no forward difference reads them).
+__device__ __forceinline__ void figure8_recip(const qt_env_params& e, double om, double st, double ct, Target& o) {
+  const double sc = e.amplitude;
+  const double den = 1.0 + st * st;
+  const double dcos = -st * om, dsin = ct * om;
+  const double dden = 2.0 * st * dsin;
+  const double r = 1.0 / den, r2 = r * r;
+  o.p[0] = e.center[0] + sc * ct * r;
+  o.p[1] = e.center[1] + sc * st * ct * r;
+  o.p[2] = e.center[2];
+  o.v[0] = sc * ((dcos * den - ct * dden) * r2);
+  o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) * r2);
+  o.v[2] = 0.0;
+  o.a[0] = o.a[1] = o.a[2] = 0.0;
+}
+
 // pattern.get_state(t) (target_motion.py:51-248) + TargetMotion.get_state's
 // acceleration clamp (403-405).  WANT_ACC = false skips the acceleration,
 // which only the feed-forward path reads (riccati_lqr.py:853-861).
@@ -156,6 +175,10 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     const int na = periodic_angles(motion, pt, t, th);
     for (int i = 0; i < na; ++i) fast_sincos(th[i], &s[i], &c[i]);
     periodic_state<WANT_ACC>(e, motion, pt, s, c, o);
+  } else if (motion == QT_MOTION_FIGURE8 && RECIP && !WANT_ACC) {
+    double st, ct;
+    fast_sincos(pt.o0 * t, &st, &ct);
+    figure8_recip(e, pt.o0, st, ct, o);
   } else if (motion == QT_MOTION_FIGURE8) {
     const double sc = e.amplitude, om = pt.o0;
     double st, ct;
@@ -164,18 +187,10 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     double dcos = -st * om, dsin = ct * om;
     double dden = 2.0 * st * dsin;
     double den2 = den * den;
-    if (RECIP && !WANT_ACC) {
-      const double r = 1.0 / den, r2 = r * r;
-      o.p[0] = e.center[0] + sc * ct * r;
-      o.p[1] = e.center[1] + sc * st * ct * r;
-      o.v[0] = sc * ((dcos * den - ct * dden) * r2);
-      o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) * r2);
-    } else {
-      o.p[0] = e.center[0] + sc * ct / den;
-      o.p[1] = e.center[1] + sc * st * ct / den;
-      o.v[0] = sc * ((dcos * den - ct * dden) / den2);
-      o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
-    }
+    o.p[0] = e.center[0] + sc * ct / den;
+    o.p[1] = e.center[1] + sc * st * ct / den;
+    o.v[0] = sc * ((dcos * den - ct * dden) / den2);
+    o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
     if (WANT_ACC) {
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;
@@ -257,7 +272,7 @@ struct Plant {
   double inv_mass, gz;
 };
 
-__device__ __forceinline__ Plant make_plant(const qt_env_params& e, double mass) {
+QT_HD Plant make_plant(const qt_env_params& e, double mass) {
   return Plant{1.0 / mass, -mass * e.gravity};
 }
 
@@ -404,7 +419,7 @@ QT_HD RateLin make_rate_lin(const qt_env_params& e) {
   return L;
 }
 
-__device__ __forceinline__ VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
+QT_HD VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
   VelLin L;
   const double h = e.dt, delta = e.drag_linear * pl.inv_mass;
   const double zero[4] = {0.0, 0.0, 0.0, 0.0};
@@ -425,6 +440,58 @@ __device__ __forceinline__ VelLin make_vel_lin(const qt_env_params& e, const Pla
   L.gv = g * sw;
   L.gp = g * sp;
   return L;
+}
+
+// Launch-level constants of the yaw-at-rest fast loop (run_yaw0), computed on
+// the host and passed as a kernel argument, so that they live in SGPRs:
+// the rate / attitude closed form, the velocity / position closed form and
+// plant constants at env.mass (launches whose plant is uniform), and the
+// rotors of the periodic target patterns: a carried sin / cos pair of an
+// angle theta_i = omega_i t + phase_i advances by the fixed rotation
+// (cos, sin)(fl(omega_i dt)) and a first-order correction by
+// omega_i ((t_new - t) - dt) + (omega_i dt - fl(omega_i dt)) (rotor_residual).
+struct LaunchConst {
+  RateLin rl;
+  VelLin vl;
+  Plant pl;
+  double rc[3], rs[3];    // cos / sin of fl(omega_i dt)
+  double om[3], ores[3];  // omega_i, omega_i dt - fl(omega_i dt)
+};
+
+// omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)
+QT_HD int pattern_omegas(const qt_env_params& e, int motion, double* om) {
+  if (motion == QT_MOTION_CIRCULAR) {
+    om[0] = e.speed / e.radius;
+    return 1;
+  }
+  if (motion == QT_MOTION_SINUSOIDAL) {
+    om[0] = 2.0 * kPi * e.frequency;
+    om[1] = 2.0 * kPi * (e.frequency * 1.3);
+    om[2] = 2.0 * kPi * (e.frequency * 0.7);
+    return 3;
+  }
+  if (motion == QT_MOTION_FIGURE8) {
+    om[0] = e.speed / e.amplitude;
+    return 1;
+  }
+  return 0;
+}
+
+inline LaunchConst make_launch_const(const qt_env_params& e, int motion) {
+  LaunchConst k{};
+  k.rl = make_rate_lin(e);
+  k.pl = make_plant(e, e.mass);
+  k.vl = make_vel_lin(e, k.pl);
+  double om[3] = {0.0, 0.0, 0.0};
+  const int na = pattern_omegas(e, motion, om);
+  for (int i = 0; i < na; ++i) {
+    const double a = om[i] * e.dt;
+    k.rc[i] = cos(a);
+    k.rs[i] = sin(a);
+    k.om[i] = om[i];
+    k.ores[i] = fma(om[i], e.dt, -a);  // exact residual of the rounded product
+  }
+  return k;
 }
 
 // Roll / pitch sin / cos carried across yaw-at-rest fast steps: the new
@@ -808,10 +875,11 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
     const double lim = c.integral_limit;
     if (FAST) {
       // the threshold gate as a step size: I + 0 e == I (up to the sign of a
-      // zero integral, which no later operation distinguishes)
+      // zero integral, which no later operation distinguishes); I + dt * e
+      // rounded as the reference rounds it (no contraction)
       const double g = em > c.integral_zero_threshold ? c.dt : 0.0;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) integ[i] = fma(g, ep[i], integ[i]);
+      for (int i = 0; i < 3; ++i) integ[i] = __dadd_rn(integ[i], __dmul_rn(g, ep[i]));
     } else if (em > c.integral_zero_threshold) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -901,7 +969,10 @@ __device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, cons
 #pragma unroll
   for (int i = 0; i < 3; ++i) ep[i] = tg.p[i] - qp[i];
   const double last = integ[3];
-  const double dt = last != last ? 0.0 : now - last;
+  // NaN = None (the first observation); a bit test, since the fast kernels are
+  // built with relaxed NaN handling (qt_rollout_fast.hip)
+  const bool none = (__double_as_longlong(last) & 0x7fffffffffffffffLL) > 0x7ff0000000000000LL;
+  const double dt = none ? 0.0 : now - last;
   integ[3] = now;
   const double lim = c.integral_limit;
   if (FAST) {  // select, not branch: the update is a handful of FMAs

@@ -1,0 +1,653 @@
+// qt_kernels.hpp — the fused closed-loop rollout kernel and the per-episode
+// containers shared by qt_rollout.hip (exact step, other kernels, C ABI) and
+// qt_rollout_fast.hip (the fast step flavours, built with relaxed NaN
+// handling: their state is finite by construction, see rollout_kernel).
+//
+// One lane = one episode.  A launch walks `nsteps` closed-loop steps with the
+// whole episode (12-state plant, target pattern constants, 4x6 / 4x9 gains,
+// LQI integral, metric accumulators) resident in registers; HBM is touched
+// only to load the state at the start of a chunk and to store it at the end.
+// Reference functions: src/quadcopter_tracking/... of the reference repo.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "qt_device.hpp"
+
+
+// Measurement-only ablation switches (scripts/ablate.sh builds timing-only
+// variants with -DQT_ABLATE=<bits>; results of such builds are wrong by
+// construction).  The product build has QT_ABLATE == 0.
+#ifndef QT_ABLATE
+#define QT_ABLATE 0
+#endif
+#define QT_ABL_METRICS 1
+#define QT_ABL_CONSTRAIN 2
+#define QT_ABL_TERMINATION 4
+#define QT_ABL_CONTROLLER 8
+#define QT_ABL_TARGET 16
+
+// Diagnostic clock-stamp build (scripts/clock_stamp.py; -DQT_CLOCK_STAMP=1):
+// lane 0 of every wave of a fast-flavour launch records s_memtime (shader
+// clock) and s_memrealtime (100 MHz) around its step loop into a buffer of
+// its own, which no other code reads; qt_debug_stamps copies it out.  The
+// product build has QT_CLOCK_STAMP == 0 and executes no stamp.
+#ifndef QT_CLOCK_STAMP
+#define QT_CLOCK_STAMP 0
+#endif
+
+namespace qtk {
+
+using namespace qt;
+
+constexpr int kBlock = 256;
+
+struct Acc {
+  double sum_e, sum_e2, max_e, sum_u, os_max, os_cur;
+  int on_pre, on_post, os_count, os_streak, prev_on, steps, viol, term;
+};
+
+__device__ __forceinline__ Acc load_acc(const double* acc, int64_t n, int64_t e) {
+  Acc a;
+  a.sum_e = acc[QT_ACC_SUM_ERR * n + e];
+  a.sum_e2 = acc[QT_ACC_SUM_ERR2 * n + e];
+  a.max_e = acc[QT_ACC_MAX_ERR * n + e];
+  a.on_pre = (int)acc[QT_ACC_ON_PRE * n + e];
+  a.on_post = (int)acc[QT_ACC_ON_POST * n + e];
+  a.sum_u = acc[QT_ACC_SUM_EFFORT * n + e];
+  a.os_count = (int)acc[QT_ACC_OS_COUNT * n + e];
+  a.os_max = acc[QT_ACC_OS_MAX * n + e];
+  a.os_cur = acc[QT_ACC_OS_CUR * n + e];
+  a.os_streak = (int)acc[QT_ACC_OS_STREAK * n + e];
+  a.prev_on = (int)acc[QT_ACC_PREV_ON * n + e];
+  a.steps = (int)acc[QT_ACC_STEPS * n + e];
+  a.viol = (int)acc[QT_ACC_VIOLATIONS * n + e];
+  a.term = (int)acc[QT_ACC_TERM * n + e];
+  return a;
+}
+
+__device__ __forceinline__ void store_acc(double* acc, int64_t n, int64_t e, const Acc& a) {
+  acc[QT_ACC_SUM_ERR * n + e] = a.sum_e;
+  acc[QT_ACC_SUM_ERR2 * n + e] = a.sum_e2;
+  acc[QT_ACC_MAX_ERR * n + e] = a.max_e;
+  acc[QT_ACC_ON_PRE * n + e] = a.on_pre;
+  acc[QT_ACC_ON_POST * n + e] = a.on_post;
+  acc[QT_ACC_SUM_EFFORT * n + e] = a.sum_u;
+  acc[QT_ACC_OS_COUNT * n + e] = a.os_count;
+  acc[QT_ACC_OS_MAX * n + e] = a.os_max;
+  acc[QT_ACC_OS_CUR * n + e] = a.os_cur;
+  acc[QT_ACC_OS_STREAK * n + e] = a.os_streak;
+  acc[QT_ACC_PREV_ON * n + e] = a.prev_on;
+  acc[QT_ACC_STEPS * n + e] = a.steps;
+  acc[QT_ACC_VIOLATIONS * n + e] = a.viol;
+  acc[QT_ACC_TERM * n + e] = a.term;
+}
+
+struct BatchDev {
+  int64_t n;
+  const int8_t* motion;
+  const double* pattern;
+  const double* plant_mass;
+  const double* hover;
+  const double* K;
+  int32_t k_cols;
+  int32_t k_per_episode;
+  const int32_t* order;
+  int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
+};
+
+__device__ __forceinline__ int64_t episode_of(const BatchDev& b, int64_t slot) {
+  return b.order ? (int64_t)b.order[slot] : slot;
+}
+
+__device__ __forceinline__ int motion_of(const BatchDev& b, const qt_env_params& e, int64_t ep) {
+  return b.motion ? (int)b.motion[ep] : e.motion;
+}
+
+__device__ __forceinline__ Pattern pattern_of(const BatchDev& b, const qt_env_params& e, int motion, int64_t ep) {
+  const int64_t n = b.n;
+  double r0 = 0, r1 = 0, r2 = 0;
+  if (b.pattern) {
+    r0 = b.pattern[0 * n + ep];
+    r1 = b.pattern[1 * n + ep];
+    r2 = b.pattern[2 * n + ep];
+  }
+  return make_pattern(e, motion, r0, r1, r2);
+}
+
+// UNI: the launch shares one gain matrix (k_per_episode == 0, checked on the
+// host): uniform addresses, scalar loads, gains in SGPRs.
+template <int KC, bool KS, bool UNI = false>
+__device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<KC, KS>& G) {
+  const int64_t m = UNI ? 1 : (b.k_per_episode ? b.n : 1);
+  const int64_t col = UNI ? 0 : (b.k_per_episode ? ep : 0);
+#pragma unroll
+  for (int j = 0; j < Gains<KC, KS>::kCount; ++j) {
+    const int idx = (KS && KC != 3) ? structured_index<KC>(j) : j;
+    G.k[j] = b.K[(int64_t)idx * m + col];
+  }
+}
+
+// Overshoot state machine of detect_overshoots (utils/metrics.py:205-261),
+// streamed over the pre-step errors: called for every step k >= 1 with the
+// on-target flag of step k (the flag of k-1 is a.prev_on).  os_streak is the
+// off-target streak while in an overshoot phase, -1 outside one.
+__device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int window) {
+  // Branch-free form of the three transitions (metrics.py:238-254).  `start`
+  // (previous step on target, this one off) and `in_phase` (previous step
+  // off target inside a phase) exclude each other.  os_cur is only read
+  // inside a phase; outside one it holds -inf after an on-target step (so a
+  // phase start takes `over` through the same max) and is otherwise unused.
+  const bool in_phase = a.os_streak >= 0;
+  const bool start = (a.prev_on > 0) && !on;
+  const bool counted = on && in_phase && a.os_streak >= window;
+  a.os_count += counted;
+  a.os_max = counted ? fmax(a.os_max, a.os_cur) : a.os_max;
+  a.os_cur = on ? -INFINITY : fmax(over, a.os_cur);
+  a.os_streak = on ? -1 : (start ? 1 : (in_phase ? a.os_streak + 1 : -1));
+}
+
+// ---------------------------------------------------------------- rollout
+
+// The closed-loop steps of one lane.  FAST: the branch-light step of
+// qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
+// takes the exact step's decisions; rare lanes/steps (speed at the
+// clamp, attitude far outside [-pi, pi), tracking error at the radius within
+// 1e-14) fall back to the exact constraint / comparison code inside the step.
+template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
+__device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
+                                          int motion, const Pattern& pt, const Plant& pl, double hover,
+                                          const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
+                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep,
+                                          const RateLin& rl) {
+  const double R = cr.target_radius;
+  const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
+  const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
+  // squared pre-step tracking error: the previous step's post-step error
+  // (same positions, same target: positions are not constrained), carried
+  double se_pre;
+  {
+    const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+    se_pre = ep0 * ep0 + ep1 * ep1 + ep2 * ep2;
+  }
+  // fast steps of a periodic pattern carry its angles' sin / cos (target_state_carried)
+  constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
+  PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
+  if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
+  // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
+  // and carried roll / pitch sin / cos (attitude_trig_advance)
+  VelLin lin;
+  Trig ta;
+  double aprev[2];
+  if constexpr (FAST && YAW0) {
+    lin = make_vel_lin(e, pl);
+    trig_of<true>(x + 6, ta);
+    aprev[0] = x[6], aprev[1] = x[7];
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    if (a.term != QT_TERM_RUNNING) break;
+    // ---- compute_action on the current observation (riccati_lqr.py:779-967)
+    double u[4];
+    // fast step: the pre-step tracking error, also the LQI's ||e_p|| (riccati_lqr.py:873)
+    const double err_fast = FAST ? sqrt_noscale(se_pre) : 0.0;
+    if (QT_ABLATE & QT_ABL_CONTROLLER) {
+      u[0] = hover, u[1] = u[2] = u[3] = 0.0;
+    } else {
+      if constexpr (KC == 3)
+        compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
+      else
+        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err_fast);
+    }
+    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
+    if (!(QT_ABLATE & QT_ABL_METRICS)) {
+      double err, un;
+      if (FAST) {
+        err = err_fast;
+        un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      } else {
+        const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
+        err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
+        un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+      }
+      a.sum_e += err;
+      a.sum_e2 += err * err;
+      if (FAST)  // err and max_e are numbers here (finite state): a plain max
+        a.max_e = fmax(a.max_e, err);
+      else if (!(err <= a.max_e) && !(a.max_e != a.max_e))
+        a.max_e = err;  // np.max, NaN-propagating
+      const bool on = err <= R;
+      a.on_pre += on;
+      a.sum_u += un;
+      overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
+      a.prev_on = on;
+    }
+    // ---- env.step (quadcopter_env.py:152-232)
+    if (FAST) {
+      // the command is finite and inside the env clamps: parsing is the identity
+      if constexpr (YAW0)
+        integrate_yaw0(rl, lin, pl, ta, x, u);
+      else
+        integrate<true, false>(e, pl, x, u);
+      t += e.dt;
+      if (!(QT_ABLATE & QT_ABL_TARGET)) {
+        if constexpr (kCarry)
+          target_state_carried<FF, MOTION>(e, pt, t, ptrig, tg);
+        else
+          target_state<FF, true>(e, motion, pt, t, tg);
+      }
+      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+      const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
+      se_pre = se;
+      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
+      // Wave-uniform choice: when any lane is off the fast preconditions the
+      // whole wave runs the exact code, which takes the fast code's decisions
+      // on the lanes that qualify.  A uniform, expected condition is a
+      // not-taken scalar branch with the exact code out of line; a divergent
+      // if / else cost a taken branch around the else block every step.
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
+        if constexpr (YAW0) attitude_trig_advance(x + 6, aprev, ta);
+        a.on_post += se < er2lo;
+      } else {  // rare: exact constraints and comparison
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
+        if constexpr (YAW0) {  // restart the carried attitude trig (|roll|, |pitch| <= pi/3 again)
+          trig_of<true>(x + 6, ta);
+          aprev[0] = x[6], aprev[1] = x[7];
+        }
+        a.on_post += norm_le(se, e.target_radius);
+      }
+      if (QT_ABLATE & QT_ABL_TERMINATION)
+        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
+      else
+        a.term = termination_fast(e, t, x);
+      a.steps += 1;
+    } else {
+      double ua[4];
+      a.viol += parse_action(e, u, ua);
+      integrate(e, pl, x, ua);
+      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
+      t += e.dt;
+      if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
+      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+      a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
+      if (QT_ABLATE & QT_ABL_TERMINATION)
+        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
+      else
+        a.term = termination(e, t, x);
+      a.steps += 1;
+      if (rec) {
+        double* r = rec + (int64_t)s * 16 * n + ep;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r[i * n] = x[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[(12 + i) * n] = u[i];
+      }
+    }
+  }
+}
+
+// Finiteness by the exponent bits: the same answer under IEEE and under the
+// fast translation unit's relaxed NaN handling (which may fold a floating
+// point isfinite or x != x), so the fast and the exact kernel take the same
+// wave decision.
+__device__ __forceinline__ bool finite_bits(double v) {
+  return (__double_as_longlong(v) & 0x7ff0000000000000LL) != 0x7ff0000000000000LL;
+}
+
+__device__ __forceinline__ bool all_finite(const double* v, int k) {
+  bool ok = true;
+  for (int i = 0; i < k; ++i) ok = ok & finite_bits(v[i]);
+  return ok;
+}
+
+// step flavours: the exact step, the fast step, the fast step with yaw at rest
+constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
+
+// ------------------------------------------------- yaw-at-rest fast loop
+
+// Sum of squares in the reference's order, ((a^2 + b^2) + c^2) without FMA
+// contraction (np.linalg.norm / the oracle's norm3): with sqrt_pos's
+// correctly rounded root, the fast loop's tracking error equals the exact
+// step's bit for bit on the same state, so its on-target and LQI-gate
+// decisions need no knife-edge band.
+__device__ __forceinline__ double sq3_ref(double a, double b, double c) {
+  return __dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c));
+}
+
+// Carried sin / cos of a periodic target's angles (circular: 1, sinusoidal:
+// 3, figure-8: theta = omega t).  Each step rotates them by the launch's
+// fixed rotor (cos, sin)(fl(omega dt)) and then by the first-order
+// correction omega ((t_new - t) - dt) + (omega dt - fl(omega dt)): the
+// carried pair follows sin / cos of omega t_k + phase for the env's
+// accumulated time t_k (t += dt, quadcopter_env.py:191) to a few ulp per
+// step, where the reference evaluates sin / cos of that angle rounded
+// (target_motion.py:86, 144, 179).
+template <int MOTION>
+struct Rotor {
+  static constexpr int NA = MOTION == QT_MOTION_SINUSOIDAL ? 3 : 1;
+  double s[NA], c[NA];
+};
+
+template <int MOTION>
+__device__ __forceinline__ void rotor_init(const Pattern& pt, double t, Rotor<MOTION>& r) {
+  double th[3];
+  if (MOTION == QT_MOTION_FIGURE8)
+    th[0] = pt.o0 * t;
+  else
+    periodic_angles(MOTION, pt, t, th);
+#pragma unroll
+  for (int i = 0; i < Rotor<MOTION>::NA; ++i) fast_sincos(th[i], &r.s[i], &r.c[i]);
+}
+
+template <int MOTION>
+__device__ __forceinline__ void rotor_advance(const LaunchConst& k, double dtt, Rotor<MOTION>& r) {
+#pragma unroll
+  for (int i = 0; i < Rotor<MOTION>::NA; ++i) {
+    const double s0 = r.s[i], c0 = r.c[i];
+    const double s1 = fma(s0, k.rc[i], c0 * k.rs[i]);
+    const double c1 = fma(c0, k.rc[i], -(s0 * k.rs[i]));
+    const double d = fma(k.om[i], dtt, k.ores[i]);
+    r.s[i] = fma(c1, d, s1);
+    r.c[i] = fma(-s1, d, c1);
+  }
+}
+
+template <bool WANT_ACC, int MOTION>
+__device__ __forceinline__ void target_from_rotor(const qt_env_params& e, const Pattern& pt, const Rotor<MOTION>& r,
+                                                  Target& o) {
+  if constexpr (MOTION == QT_MOTION_FIGURE8) {
+    figure8_recip(e, pt.o0, r.s[0], r.c[0], o);  // no feed-forward: no acceleration
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o.p[i] = e.center[i], o.v[i] = 0.0, o.a[i] = 0.0;
+    periodic_state<WANT_ACC>(e, MOTION, pt, r.s, r.c, o);
+    if (WANT_ACC) clamp_acceleration(e, o);
+  }
+}
+
+// The env's velocity clamp (quadcopter_env.py:442-445) alone: the only part
+// of _apply_state_constraints that a yaw-at-rest fast step can need beyond
+// constrain_fast_apply (rates stay inside their clamp, angles inside the
+// wrap's range: rate_bounded_ok, trig_of<true>).
+__device__ __forceinline__ void clamp_velocity(const qt_env_params& e, double* x) {
+  const double s = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
+  if (norm_gt(s, e.max_velocity)) {
+    const double vm = sqrt(s);
+#pragma unroll
+    for (int i = 3; i < 6; ++i) x[i] = x[i] / vm * e.max_velocity;
+  }
+}
+
+// The yaw-at-rest fast loop (flavour kYaw0).  One wave-uniform loop: every
+// step runs branch-free (closed-form RK4, carried roll / pitch and target
+// trig, fused metrics) and ends with ONE wave vote; the loop leaves only when
+// some lane needs the exact velocity clamp, terminates (time limit, position
+// bounds) or the chunk ends.  Such a step is then finished exactly (the
+// velocity clamp, per-lane termination) and the loop restarts for the lanes
+// still running, so a wave pays no per-lane exec-mask bookkeeping and one
+// taken branch (the back edge) per step.
+// Overshoot state machine (detect_overshoots, utils/metrics.py:205-261) as
+// one counter z: 1 after an on-target step, k + 1 in an off-target phase of
+// length k that began on->off, <= 0 off target outside a phase; a phase's
+// running maximum `cur` restarts at the on-target step's err - R <= 0, which
+// any off-target excess > 0 replaces.
+template <int MOTION, int KC, bool FF, bool KS, bool UNI>
+__device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
+                                         int motion, const Pattern& pt, const Plant& pl_lane, double hover,
+                                         const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
+                                         Acc& a, int nsteps, const LaunchConst& k) {
+  constexpr bool kRotor = MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
+                          (MOTION == QT_MOTION_FIGURE8 && !FF);
+  constexpr int kNeg = -(1 << 30);
+  const Plant pl = UNI ? k.pl : pl_lane;
+  const VelLin lin = UNI ? k.vl : make_vel_lin(e, pl_lane);
+  const double R = cr.target_radius, eR = e.target_radius;
+  const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
+  const int W = cr.overshoot_window;
+  int s = 0;
+  while (a.term == QT_TERM_RUNNING && s < nsteps) {
+    // (re)start: the pre-step tracking error of the current observation,
+    // roll / pitch trig, target rotor, overshoot counter
+    // The observation is re-derived from t (the stored one is the same
+    // function of t), so that loop-invariant target rows (a linear target's
+    // velocity) stay invariant in registers.
+    Rotor<kRotor ? MOTION : QT_MOTION_CIRCULAR> rot;
+    if constexpr (kRotor) {
+      rotor_init<MOTION>(pt, t, rot);
+      target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+    } else {
+      target_state<FF, true>(e, motion, pt, t, tg);
+    }
+    double err = sqrt_pos(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
+    Trig ta;
+    trig_of<true>(x + 6, ta);
+    int z = a.prev_on == 1 ? 1 : (a.os_streak >= 0 ? a.os_streak + 1 : kNeg);
+    double cur = a.os_cur;
+    int on_pre = a.on_pre, on_post = a.on_post, os_count = a.os_count;
+    const int s0 = s;
+    const int s_end = nsteps - s0 > (1 << 29) ? s0 + (1 << 29) : nsteps;  // z stays < 1 off phase
+    bool rare = false;
+    do {
+      const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_advance)
+      // ---- compute_action on the current observation (riccati_lqr.py:779-967)
+      double u[4];
+      if (QT_ABLATE & QT_ABL_CONTROLLER) {
+        u[0] = hover, u[1] = u[2] = u[3] = 0.0;
+      } else {
+        if constexpr (KC == 3)
+          compute_action_pid<FF, true>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
+        else
+          compute_action<KC, FF, KS, true>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err);
+      }
+      // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics
+      if (!(QT_ABLATE & QT_ABL_METRICS)) {
+        a.sum_e += err;
+        a.sum_e2 = fma(err, err, a.sum_e2);
+        a.max_e = fmax(a.max_e, err);
+        const bool on = err <= R;
+        on_pre += on;
+        a.sum_u += sqrt_sum(fma(u[2], u[2], fma(u[1], u[1], u[0] * u[0])));  // u[3] = 0: no yaw command
+        const bool counted = on & (z > W);
+        os_count += counted;
+        a.os_max = counted ? fmax(a.os_max, cur) : a.os_max;
+        cur = on ? err - R : fmax(cur, err - R);
+        z = on ? 1 : z + 1;
+      }
+      // ---- env.step (quadcopter_env.py:152-232): the command is finite and
+      // inside the env clamps, so parsing is the identity
+      integrate_yaw0(k.rl, lin, pl, ta, x, u);
+      const double t0 = t;
+      t += e.dt;
+      if (!(QT_ABLATE & QT_ABL_TARGET)) {
+        if constexpr (kRotor) {
+          rotor_advance<MOTION>(k, (t - t0) - e.dt, rot);
+          target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+        } else {
+          target_state<FF, true>(e, motion, pt, t, tg);
+        }
+      }
+      // post-step tracking error: the env's on-target count now, the next
+      // step's pre-step error (positions are not constrained)
+      err = sqrt_pos(sq3_ref(x[0] - tg.p[0], x[1] - tg.p[1], x[2] - tg.p[2]));
+      on_post += err <= eR;
+      const bool vbad = !(x[3] * x[3] + x[4] * x[4] + x[5] * x[5] < vm2);
+      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
+      double ap[2] = {a0[0], a0[1]};
+      attitude_trig_advance(x + 6, ap, ta);
+      const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
+      const bool tl = t >= e.max_episode_time;
+      ++s;
+      // one vote: each compare's lane mask, or-ed on the scalar unit
+      rare = (__builtin_amdgcn_ballot_w64(vbad) | __builtin_amdgcn_ballot_w64(pb) |
+              __builtin_amdgcn_ballot_w64(tl)) != 0;
+    } while (!rare && s < s_end);
+    a.steps += s - s0;
+    a.on_pre = on_pre, a.on_post = on_post, a.os_count = os_count;
+    a.prev_on = z == 1 ? 1 : 0;
+    a.os_streak = z >= 2 ? z - 1 : -1;
+    a.os_cur = cur;
+    if (rare) {  // finish the last step exactly
+      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) clamp_velocity(e, x);
+      a.term = (QT_ABLATE & QT_ABL_TERMINATION) ? (t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING)
+                                                 : termination_fast(e, t, x);
+    }
+  }
+}
+
+// MOTION >= 0 specialises the target pattern; -1 reads it per episode.
+// UNI (fast flavours): no per-episode mass, hover thrust or gains — the
+// plant constants come from the launch (LaunchConst) and the gains from
+// uniform addresses, all in SGPRs (checked on the host, launch_rollout).
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
+__global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+                                                         BatchDev b, qt_state st, int nsteps,
+                                                         double* __restrict__ rec, int deferred, LaunchConst lc) {
+  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.slot_end) return;
+  const int64_t n = b.n, ep = episode_of(b, slot);
+  const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
+  const Pattern pt = pattern_of(b, e, motion, ep);
+  const Plant pl = UNI ? lc.pl : make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
+  const double hover = UNI ? c.hover_thrust : (b.hover ? b.hover[ep] : c.hover_thrust);
+  Gains<KC, KS> G;
+  load_gains<KC, KS, UNI>(b, ep, G);
+
+  // integ: LQI integral (KC 9) | PID integral error + last observation time (KC 3)
+  constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
+  double x[12], integ[4] = {0, 0, 0, 0};  // PID: row 3 (last observation time) is loaded
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) integ[i] = st.integ[i * n + ep];
+  Target tg;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    tg.p[i] = st.target[i * n + ep];
+    tg.v[i] = st.target[(3 + i) * n + ep];
+    tg.a[i] = st.target[(6 + i) * n + ep];
+  }
+  double t = st.t[ep];
+  Acc a = load_acc(st.acc, n, ep);
+
+  // Which step the wavefront runs (uniform).  A fast flavour is launched only
+  // when the launch-level preconditions hold (fast_path_ok, no recording); it
+  // takes the waves whose lanes all qualify and leaves the others untouched,
+  // and the exact kernel launched after it with `deferred` = that flavour
+  // takes exactly those (the same test on the same inputs).
+  // (every comparison below is taken on values the bit tests proved finite)
+  bool lane_ok = a.term != QT_TERM_RUNNING ||
+                 (all_finite(G.k, Gains<KC, KS>::kCount) && all_finite(x, 12) && all_finite(integ, 3) &&
+                  all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && finite_bits(hover) &&
+                  finite_bits(pl.inv_mass) && finite_bits(t) && fabs(t) < 1e300);
+  for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
+  // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
+  // never command yaw: a yaw at rest stays exactly zero
+  // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
+  // rate-bounded, roll and pitch rates within the command clip: rate_bounded_ok)
+  if (FLAVOR == kYaw0 || deferred == kYaw0)
+    lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0 && fabs(x[6]) <= kMaxTilt && fabs(x[7]) <= kMaxTilt &&
+              fabs(x[9]) <= c.max_rate && fabs(x[10]) <= c.max_rate;
+  const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
+  if (FLAVOR != kExact) {
+    if (!wave_ok) return;
+#if QT_CLOCK_STAMP && defined(QT_FAST_TU)
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if constexpr (FLAVOR == kYaw0)
+      run_yaw0<MOTION, KC, FF, KS, UNI>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, lc);
+    else
+      run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps,
+                                                 rec, n, ep, lc.rl);
+#if QT_CLOCK_STAMP && defined(QT_FAST_TU)
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    const int64_t wave = (slot - b.slot0) >> 6;
+    if ((threadIdx.x & 63) == 0 && wave < kStampWaves) {
+      g_qt_stamps[wave][0] = t0, g_qt_stamps[wave][1] = t1;
+      g_qt_stamps[wave][2] = r0, g_qt_stamps[wave][3] = r1;
+    }
+#endif
+  } else {
+    if (deferred != kExact && wave_ok) return;
+    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
+                                                n, ep, lc.rl);
+  }
+  // Without feed-forward the loop leaves the acceleration rows at zero (only
+  // feed-forward reads them); the stored observation carries the reference's
+  // acceleration (target_motion.py:387-411) for later chunks and callers.
+  if (!FF && (motion == QT_MOTION_CIRCULAR || motion == QT_MOTION_SINUSOIDAL || motion == QT_MOTION_FIGURE8)) {
+    Target full;
+    target_state<true>(e, motion, pt, t, full);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tg.a[i] = full.a[i];
+  }
+
+#pragma unroll
+  for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    st.target[i * n + ep] = tg.p[i];
+    st.target[(3 + i) * n + ep] = tg.v[i];
+    st.target[(6 + i) * n + ep] = tg.a[i];
+  }
+  st.t[ep] = t;
+  store_acc(st.acc, n, ep, a);
+}
+
+inline BatchDev to_dev(const qt_batch* b) {
+  return BatchDev{b->n,     b->motion,        b->pattern, b->plant_mass, b->hover_thrust, b->K,
+                  b->k_cols, b->k_per_episode, b->order,   0,             b->n};
+}
+
+inline int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+
+inline int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
+
+inline bool valid_state(const qt_state& st, bool need_integ) {
+  return st.x && st.t && st.acc && st.target && (!need_integ || st.integ);
+}
+
+// Fast step flavours (qt_rollout_fast.hip): launches rollout_kernel<flavor>
+// (kFast or kYaw0) for the runtime controller / target choice.
+// uni: no per-episode mass, hover thrust or gains (rollout_kernel's UNI).
+void launch_fast(int flavor, bool uni, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
+                 const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
+                 const qt_state& st, int nsteps, const LaunchConst& lc);
+
+// Calls L::template run<MOTION, KC, FF, KS>(args...) for a runtime (kc, ff, ks, motion);
+// PID (kc 3) never commands yaw and always takes the structured form.
+template <class L, int KC, bool FF, bool KS, class... A>
+void dispatch_motion(int motion, A&&... args) {
+  switch (motion) {
+    case QT_MOTION_STATIONARY: L::template run<QT_MOTION_STATIONARY, KC, FF, KS>(args...); break;
+    case QT_MOTION_LINEAR: L::template run<QT_MOTION_LINEAR, KC, FF, KS>(args...); break;
+    case QT_MOTION_CIRCULAR: L::template run<QT_MOTION_CIRCULAR, KC, FF, KS>(args...); break;
+    case QT_MOTION_SINUSOIDAL: L::template run<QT_MOTION_SINUSOIDAL, KC, FF, KS>(args...); break;
+    case QT_MOTION_FIGURE8: L::template run<QT_MOTION_FIGURE8, KC, FF, KS>(args...); break;
+    default: L::template run<-1, KC, FF, KS>(args...);
+  }
+}
+
+template <class L, int KC, class... A>
+void dispatch_ffks(bool ff, bool ks, int motion, A&&... args) {
+  if constexpr (KC == 3) {
+    if (ff) dispatch_motion<L, 3, true, true>(motion, args...);
+    else dispatch_motion<L, 3, false, true>(motion, args...);
+  } else if (ff) {
+    if (ks) dispatch_motion<L, KC, true, true>(motion, args...);
+    else dispatch_motion<L, KC, true, false>(motion, args...);
+  } else {
+    if (ks) dispatch_motion<L, KC, false, true>(motion, args...);
+    else dispatch_motion<L, KC, false, false>(motion, args...);
+  }
+}
+
+template <class L, class... A>
+void dispatch_rollout(int kc, bool ff, bool ks, int motion, A&&... args) {
+  if (kc == 9) dispatch_ffks<L, 9>(ff, ks, motion, args...);
+  else if (kc == 3) dispatch_ffks<L, 3>(ff, ks, motion, args...);
+  else dispatch_ffks<L, 6>(ff, ks, motion, args...);
+}
+
+}  // namespace qtk
+

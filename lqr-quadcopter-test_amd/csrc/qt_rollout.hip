@@ -4,144 +4,14 @@
 // whole episode (12-state plant, target pattern constants, 4x6 / 4x9 gains,
 // LQI integral, metric accumulators) resident in registers; HBM is touched
 // only to load the state at the start of a chunk and to store it at the end.
+// The rollout kernel itself lives in qt_kernels.hpp; its fast flavours are
+// instantiated in qt_rollout_fast.hip.
 // Reference functions: src/quadcopter_tracking/... of the reference repo.
-#include <hip/hip_runtime.h>
+#include "qt_kernels.hpp"
 
-#include "qt_device.hpp"
-
-using namespace qt;
-
-// Measurement-only ablation switches (scripts/ablate.sh builds timing-only
-// variants with -DQT_ABLATE=<bits>; results of such builds are wrong by
-// construction).  The product build has QT_ABLATE == 0.
-#ifndef QT_ABLATE
-#define QT_ABLATE 0
-#endif
-#define QT_ABL_METRICS 1
-#define QT_ABL_CONSTRAIN 2
-#define QT_ABL_TERMINATION 4
-#define QT_ABL_CONTROLLER 8
-#define QT_ABL_TARGET 16
-
-// Diagnostic clock-stamp build (scripts/clock_stamp.py; -DQT_CLOCK_STAMP=1):
-// lane 0 of every wave of a fast-flavour launch records s_memtime (shader
-// clock) and s_memrealtime (100 MHz) around its step loop into a buffer of
-// its own, which no other code reads; qt_debug_stamps copies it out.  The
-// product build has QT_CLOCK_STAMP == 0 and executes no stamp.
-#ifndef QT_CLOCK_STAMP
-#define QT_CLOCK_STAMP 0
-#endif
-#if QT_CLOCK_STAMP
-constexpr int kStampWaves = 1 << 16;
-__device__ unsigned long long g_qt_stamps[kStampWaves][4];
-#endif
+using namespace qtk;
 
 namespace {
-
-constexpr int kBlock = 256;
-
-struct Acc {
-  double sum_e, sum_e2, max_e, sum_u, os_max, os_cur;
-  int on_pre, on_post, os_count, os_streak, prev_on, steps, viol, term;
-};
-
-__device__ __forceinline__ Acc load_acc(const double* acc, int64_t n, int64_t e) {
-  Acc a;
-  a.sum_e = acc[QT_ACC_SUM_ERR * n + e];
-  a.sum_e2 = acc[QT_ACC_SUM_ERR2 * n + e];
-  a.max_e = acc[QT_ACC_MAX_ERR * n + e];
-  a.on_pre = (int)acc[QT_ACC_ON_PRE * n + e];
-  a.on_post = (int)acc[QT_ACC_ON_POST * n + e];
-  a.sum_u = acc[QT_ACC_SUM_EFFORT * n + e];
-  a.os_count = (int)acc[QT_ACC_OS_COUNT * n + e];
-  a.os_max = acc[QT_ACC_OS_MAX * n + e];
-  a.os_cur = acc[QT_ACC_OS_CUR * n + e];
-  a.os_streak = (int)acc[QT_ACC_OS_STREAK * n + e];
-  a.prev_on = (int)acc[QT_ACC_PREV_ON * n + e];
-  a.steps = (int)acc[QT_ACC_STEPS * n + e];
-  a.viol = (int)acc[QT_ACC_VIOLATIONS * n + e];
-  a.term = (int)acc[QT_ACC_TERM * n + e];
-  return a;
-}
-
-__device__ __forceinline__ void store_acc(double* acc, int64_t n, int64_t e, const Acc& a) {
-  acc[QT_ACC_SUM_ERR * n + e] = a.sum_e;
-  acc[QT_ACC_SUM_ERR2 * n + e] = a.sum_e2;
-  acc[QT_ACC_MAX_ERR * n + e] = a.max_e;
-  acc[QT_ACC_ON_PRE * n + e] = a.on_pre;
-  acc[QT_ACC_ON_POST * n + e] = a.on_post;
-  acc[QT_ACC_SUM_EFFORT * n + e] = a.sum_u;
-  acc[QT_ACC_OS_COUNT * n + e] = a.os_count;
-  acc[QT_ACC_OS_MAX * n + e] = a.os_max;
-  acc[QT_ACC_OS_CUR * n + e] = a.os_cur;
-  acc[QT_ACC_OS_STREAK * n + e] = a.os_streak;
-  acc[QT_ACC_PREV_ON * n + e] = a.prev_on;
-  acc[QT_ACC_STEPS * n + e] = a.steps;
-  acc[QT_ACC_VIOLATIONS * n + e] = a.viol;
-  acc[QT_ACC_TERM * n + e] = a.term;
-}
-
-struct BatchDev {
-  int64_t n;
-  const int8_t* motion;
-  const double* pattern;
-  const double* plant_mass;
-  const double* hover;
-  const double* K;
-  int32_t k_cols;
-  int32_t k_per_episode;
-  const int32_t* order;
-  int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
-};
-
-__device__ __forceinline__ int64_t episode_of(const BatchDev& b, int64_t slot) {
-  return b.order ? (int64_t)b.order[slot] : slot;
-}
-
-__device__ __forceinline__ int motion_of(const BatchDev& b, const qt_env_params& e, int64_t ep) {
-  return b.motion ? (int)b.motion[ep] : e.motion;
-}
-
-__device__ __forceinline__ Pattern pattern_of(const BatchDev& b, const qt_env_params& e, int motion, int64_t ep) {
-  const int64_t n = b.n;
-  double r0 = 0, r1 = 0, r2 = 0;
-  if (b.pattern) {
-    r0 = b.pattern[0 * n + ep];
-    r1 = b.pattern[1 * n + ep];
-    r2 = b.pattern[2 * n + ep];
-  }
-  return make_pattern(e, motion, r0, r1, r2);
-}
-
-template <int KC, bool KS>
-__device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<KC, KS>& G) {
-  const int64_t m = b.k_per_episode ? b.n : 1;
-  const int64_t col = b.k_per_episode ? ep : 0;  // shared: uniform address -> scalar loads
-#pragma unroll
-  for (int j = 0; j < Gains<KC, KS>::kCount; ++j) {
-    const int idx = (KS && KC != 3) ? structured_index<KC>(j) : j;
-    G.k[j] = b.K[(int64_t)idx * m + col];
-  }
-}
-
-// Overshoot state machine of detect_overshoots (utils/metrics.py:205-261),
-// streamed over the pre-step errors: called for every step k >= 1 with the
-// on-target flag of step k (the flag of k-1 is a.prev_on).  os_streak is the
-// off-target streak while in an overshoot phase, -1 outside one.
-__device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int window) {
-  // Branch-free form of the three transitions (metrics.py:238-254).  `start`
-  // (previous step on target, this one off) and `in_phase` (previous step
-  // off target inside a phase) exclude each other.  os_cur is only read
-  // inside a phase; outside one it holds -inf after an on-target step (so a
-  // phase start takes `over` through the same max) and is otherwise unused.
-  const bool in_phase = a.os_streak >= 0;
-  const bool start = (a.prev_on > 0) && !on;
-  const bool counted = on && in_phase && a.os_streak >= window;
-  a.os_count += counted;
-  a.os_max = counted ? fmax(a.os_max, a.os_cur) : a.os_max;
-  a.os_cur = on ? -INFINITY : fmax(over, a.os_cur);
-  a.os_streak = on ? -1 : (start ? 1 : (in_phase ? a.os_streak + 1 : -1));
-}
 
 // ------------------------------------------------------------------ reset
 
@@ -171,239 +41,6 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(qt_env_params e, BatchDev
     st.target[(6 + i) * n + ep] = tg.a[i];
   }
   Acc a{0, 0, -INFINITY, 0, 0, 0, 0, 0, 0, -1, -1, 0, 0, QT_TERM_RUNNING};
-  store_acc(st.acc, n, ep, a);
-}
-
-// ---------------------------------------------------------------- rollout
-
-// The closed-loop steps of one lane.  FAST: the branch-light step of
-// qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
-// takes the exact step's decisions; rare lanes/steps (speed at the
-// clamp, attitude far outside [-pi, pi), tracking error at the radius within
-// 1e-14) fall back to the exact constraint / comparison code inside the step.
-template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
-__device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
-                                          int motion, const Pattern& pt, const Plant& pl, double hover,
-                                          const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
-                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep,
-                                          const RateLin& rl) {
-  const double R = cr.target_radius;
-  const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
-  const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
-  // squared pre-step tracking error: the previous step's post-step error
-  // (same positions, same target: positions are not constrained), carried
-  double se_pre;
-  {
-    const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-    se_pre = ep0 * ep0 + ep1 * ep1 + ep2 * ep2;
-  }
-  // fast steps of a periodic pattern carry its angles' sin / cos (target_state_carried)
-  constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
-  PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
-  if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
-  // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
-  // and carried roll / pitch sin / cos (attitude_trig_advance)
-  VelLin lin;
-  Trig ta;
-  double aprev[2];
-  if constexpr (FAST && YAW0) {
-    lin = make_vel_lin(e, pl);
-    trig_of<true>(x + 6, ta);
-    aprev[0] = x[6], aprev[1] = x[7];
-  }
-  for (int s = 0; s < nsteps; ++s) {
-    if (a.term != QT_TERM_RUNNING) break;
-    // ---- compute_action on the current observation (riccati_lqr.py:779-967)
-    double u[4];
-    // fast step: the pre-step tracking error, also the LQI's ||e_p|| (riccati_lqr.py:873)
-    const double err_fast = FAST ? sqrt_noscale(se_pre) : 0.0;
-    if (QT_ABLATE & QT_ABL_CONTROLLER) {
-      u[0] = hover, u[1] = u[2] = u[3] = 0.0;
-    } else {
-      if constexpr (KC == 3)
-        compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
-      else
-        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err_fast);
-    }
-    // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
-    if (!(QT_ABLATE & QT_ABL_METRICS)) {
-      double err, un;
-      if (FAST) {
-        err = err_fast;
-        un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
-      } else {
-        const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-        err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
-        un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
-      }
-      a.sum_e += err;
-      a.sum_e2 += err * err;
-      if (FAST)  // err and max_e are numbers here (finite state): a plain max
-        a.max_e = fmax(a.max_e, err);
-      else if (!(err <= a.max_e) && !(a.max_e != a.max_e))
-        a.max_e = err;  // np.max, NaN-propagating
-      const bool on = err <= R;
-      a.on_pre += on;
-      a.sum_u += un;
-      overshoot_step(a, on, err - R, cr.overshoot_window);  // no-op on the first step (prev_on < 0)
-      a.prev_on = on;
-    }
-    // ---- env.step (quadcopter_env.py:152-232)
-    if (FAST) {
-      // the command is finite and inside the env clamps: parsing is the identity
-      if constexpr (YAW0)
-        integrate_yaw0(rl, lin, pl, ta, x, u);
-      else
-        integrate<true, false>(e, pl, x, u);
-      t += e.dt;
-      if (!(QT_ABLATE & QT_ABL_TARGET)) {
-        if constexpr (kCarry)
-          target_state_carried<FF, MOTION>(e, pt, t, ptrig, tg);
-        else
-          target_state<FF, true>(e, motion, pt, t, tg);
-      }
-      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
-      const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
-      se_pre = se;
-      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
-      // Wave-uniform choice: when any lane is off the fast preconditions the
-      // whole wave runs the exact code, which takes the fast code's decisions
-      // on the lanes that qualify.  A uniform, expected condition is a
-      // not-taken scalar branch with the exact code out of line; a divergent
-      // if / else cost a taken branch around the else block every step.
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
-        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
-        if constexpr (YAW0) attitude_trig_advance(x + 6, aprev, ta);
-        a.on_post += se < er2lo;
-      } else {  // rare: exact constraints and comparison
-        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
-        if constexpr (YAW0) {  // restart the carried attitude trig (|roll|, |pitch| <= pi/3 again)
-          trig_of<true>(x + 6, ta);
-          aprev[0] = x[6], aprev[1] = x[7];
-        }
-        a.on_post += norm_le(se, e.target_radius);
-      }
-      if (QT_ABLATE & QT_ABL_TERMINATION)
-        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
-      else
-        a.term = termination_fast(e, t, x);
-      a.steps += 1;
-    } else {
-      double ua[4];
-      a.viol += parse_action(e, u, ua);
-      integrate(e, pl, x, ua);
-      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
-      t += e.dt;
-      if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
-      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
-      a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
-      if (QT_ABLATE & QT_ABL_TERMINATION)
-        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
-      else
-        a.term = termination(e, t, x);
-      a.steps += 1;
-      if (rec) {
-        double* r = rec + (int64_t)s * 16 * n + ep;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) r[i * n] = x[i];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[(12 + i) * n] = u[i];
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ bool all_finite(const double* v, int k) {
-  double s = 0.0;
-  for (int i = 0; i < k; ++i) s += v[i] * 0.0;  // NaN iff some v[i] is NaN or infinite
-  return s == 0.0;
-}
-
-// step flavours: the exact step, the fast step, the fast step with yaw at rest
-constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
-
-// MOTION >= 0 specialises the target pattern; -1 reads it per episode.
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS>
-__global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
-                                                         BatchDev b, qt_state st, int nsteps,
-                                                         double* __restrict__ rec, int deferred, RateLin rl) {
-  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= b.slot_end) return;
-  const int64_t n = b.n, ep = episode_of(b, slot);
-  const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
-  const Pattern pt = pattern_of(b, e, motion, ep);
-  const Plant pl = make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
-  const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
-  Gains<KC, KS> G;
-  load_gains<KC, KS>(b, ep, G);
-
-  // integ: LQI integral (KC 9) | PID integral error + last observation time (KC 3)
-  constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
-  double x[12], integ[4] = {0, 0, 0, NAN};
-#pragma unroll
-  for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) integ[i] = st.integ[i * n + ep];
-  Target tg;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    tg.p[i] = st.target[i * n + ep];
-    tg.v[i] = st.target[(3 + i) * n + ep];
-    tg.a[i] = st.target[(6 + i) * n + ep];
-  }
-  double t = st.t[ep];
-  Acc a = load_acc(st.acc, n, ep);
-
-  // Which step the wavefront runs (uniform).  A fast flavour is launched only
-  // when the launch-level preconditions hold (fast_path_ok, no recording); it
-  // takes the waves whose lanes all qualify and leaves the others untouched,
-  // and the exact kernel launched after it with `deferred` = that flavour
-  // takes exactly those (the same test on the same inputs).
-  bool lane_ok = a.term != QT_TERM_RUNNING ||
-                 (all_finite(G.k, Gains<KC, KS>::kCount) && all_finite(x, 12) && all_finite(integ, 3) &&
-                  all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && isfinite(hover) &&
-                  isfinite(pl.inv_mass) && fabs(t) < 1e300);
-  for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
-  // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
-  // never command yaw: a yaw at rest stays exactly zero
-  // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
-  // rate-bounded, roll and pitch rates within the command clip: rate_bounded_ok)
-  if (FLAVOR == kYaw0 || deferred == kYaw0)
-    lane_ok = lane_ok && x[8] == 0.0 && x[11] == 0.0 && fabs(x[6]) <= kMaxTilt && fabs(x[7]) <= kMaxTilt &&
-              fabs(x[9]) <= c.max_rate && fabs(x[10]) <= c.max_rate;
-  const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
-  if (FLAVOR != kExact) {
-    if (!wave_ok) return;
-#if QT_CLOCK_STAMP
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    run_steps<true, FLAVOR == kYaw0, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a,
-                                                         nsteps, rec, n, ep, rl);
-#if QT_CLOCK_STAMP
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    const int64_t wave = (slot - b.slot0) >> 6;
-    if ((threadIdx.x & 63) == 0 && wave < kStampWaves) {
-      g_qt_stamps[wave][0] = t0, g_qt_stamps[wave][1] = t1;
-      g_qt_stamps[wave][2] = r0, g_qt_stamps[wave][3] = r1;
-    }
-#endif
-  } else {
-    if (deferred != kExact && wave_ok) return;
-    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
-                                                n, ep, rl);
-  }
-
-#pragma unroll
-  for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    st.target[i * n + ep] = tg.p[i];
-    st.target[(3 + i) * n + ep] = tg.v[i];
-    st.target[(6 + i) * n + ep] = tg.a[i];
-  }
-  st.t[ep] = t;
   store_acc(st.acc, n, ep, a);
 }
 
@@ -731,80 +368,37 @@ __global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, co
   sum_block_reduce(p, out);
 }
 
-BatchDev to_dev(const qt_batch* b) {
-  return BatchDev{b->n,     b->motion,        b->pattern, b->plant_mass, b->hover_thrust, b->K,
-                  b->k_cols, b->k_per_episode, b->order,   0,             b->n};
-}
-
-int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
-
-int check_launch() { return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH; }
-
-template <int MOTION, int KC, bool FF, bool KS>
-void launch_flavours(bool fast, bool no_yaw, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
-                     const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec) {
-  const RateLin rl = make_rate_lin(e);  // yaw-at-rest closed-form RK4 (integrate_yaw0)
-  if (fast && (KS || no_yaw) && rate_bounded_ok(e, c)) {
-    rollout_kernel<kYaw0, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kYaw0, rl);
-  } else if (fast) {
-    rollout_kernel<kFast, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kFast, rl);
-  } else {
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, kExact, rl);
+// The exact step (also the deferred pass after a fast flavour: it takes the
+// waves the fast kernel left, see rollout_kernel).
+struct ExactLaunch {
+  template <int MOTION, int KC, bool FF, bool KS>
+  static void run(int deferred, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                  const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec,
+                  const LaunchConst& lc) {
+    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, deferred, lc);
   }
-}
+};
 
-template <int KC, bool FF, bool KS>
-void launch_rollout_motion(int motion, bool fast, bool no_yaw, int grid, hipStream_t s, const qt_env_params& e,
-                           const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st,
-                           int nsteps, double* rec) {
-  switch (motion) {
-    case QT_MOTION_STATIONARY:
-      launch_flavours<QT_MOTION_STATIONARY, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-      break;
-    case QT_MOTION_LINEAR:
-      launch_flavours<QT_MOTION_LINEAR, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-      break;
-    case QT_MOTION_CIRCULAR:
-      launch_flavours<QT_MOTION_CIRCULAR, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-      break;
-    case QT_MOTION_SINUSOIDAL:
-      launch_flavours<QT_MOTION_SINUSOIDAL, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-      break;
-    case QT_MOTION_FIGURE8:
-      launch_flavours<QT_MOTION_FIGURE8, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-      break;
-    default:
-      launch_flavours<-1, KC, FF, KS>(fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-  }
-}
-
-template <int KC>
-void launch_rollout(bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
-                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
-                    double* rec) {
+// One rollout launch set: the fast flavour the launch-level preconditions
+// allow, then the exact kernel for the waves it left (or for everything).
+int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
+                   const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
+                   double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
-  if constexpr (KC == 3) {  // PID never commands yaw (controllers/__init__.py:373): the yaw-at-rest flavour applies
-    if (ff)
-      launch_rollout_motion<3, true, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-    else
-      launch_rollout_motion<3, false, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-  } else if (ff) {
-    if (ks)
-      launch_rollout_motion<KC, true, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-    else
-      launch_rollout_motion<KC, true, false>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-  } else {
-    if (ks)
-      launch_rollout_motion<KC, false, true>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
-    else
-      launch_rollout_motion<KC, false, false>(motion, fast, no_yaw, grid, s, e, c, cr, b, st, nsteps, rec);
+  const LaunchConst lc = make_launch_const(e, motion);  // yaw-at-rest closed forms, target rotors
+  const bool ks_eff = ks || kc == 3;
+  const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
+  int flavor = kExact;
+  if (fast && (ks_eff || no_yaw) && rate_bounded_ok(e, c))
+    flavor = kYaw0;
+  else if (fast)
+    flavor = kFast;
+  if (flavor != kExact) {
+    launch_fast(flavor, uni, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
+    if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
   }
-}
-
-bool valid_state(const qt_state& st, bool need_integ) {
-  return st.x && st.t && st.acc && st.target && (!need_integ || st.integ);
+  dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, motion, flavor, grid, s, e, c, cr, b, st, nsteps, rec, lc);
+  return check_launch();
 }
 
 }  // namespace
@@ -813,16 +407,6 @@ extern "C" {
 
 int qt_abi_version(void) { return QT_ABI_VERSION; }
 
-#if QT_CLOCK_STAMP
-// Diagnostic build only: copy the first `waves` stamp records
-// {memtime start, end, realtime start, end} to host memory out[waves][4].
-int qt_debug_stamps(unsigned long long* out, int64_t waves) {
-  if (!out || waves < 0 || waves > kStampWaves) return QT_EINVAL;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 4 * waves) == hipSuccess
-             ? QT_OK
-             : QT_ELAUNCH;
-}
-#endif
 
 int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, qt_state st, void* stream) {
   if (!env || !batch || batch->n < 0) return QT_EINVAL;
@@ -845,13 +429,7 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   const bool ff = ctrl->feedforward_enabled != 0;
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
-  if (batch->k_cols == 9)
-    launch_rollout<9>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-  else if (batch->k_cols == 3)
-    launch_rollout<3>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-  else
-    launch_rollout<6>(ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-  return check_launch();
+  return launch_rollout(batch->k_cols, ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
 }
 
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
@@ -878,13 +456,9 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
     b.slot_end = seg_end[i];
     if (b.slot_end == b.slot0) continue;
     const int grid = grid_of(b.slot_end - b.slot0);
-    if (batch->k_cols == 9)
-      launch_rollout<9>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-    else if (batch->k_cols == 3)
-      launch_rollout<3>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-    else
-      launch_rollout<6>(ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
-    if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
+    if (launch_rollout(batch->k_cols, ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps,
+                       rec) != QT_OK)
+      return QT_ELAUNCH;
   }
   return QT_OK;
 }
