@@ -448,14 +448,14 @@ QT_HD VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
 // plant constants at env.mass (launches whose plant is uniform), and the
 // rotors of the periodic target patterns: a carried sin / cos pair of an
 // angle theta_i = omega_i t + phase_i advances by the fixed rotation
-// (cos, sin)(fl(omega_i dt)) and a first-order correction by
-// omega_i ((t_new - t) - dt) + (omega_i dt - fl(omega_i dt)) (rotor_residual).
+// (cos, sin)(fl(omega_i dt)) and omega_i times the time step's rounding each
+// step (qt_kernels.hpp, Rotor).
 struct LaunchConst {
   RateLin rl;
   VelLin vl;
   Plant pl;
-  double rc[3], rs[3];    // cos / sin of fl(omega_i dt)
-  double om[3], ores[3];  // omega_i, omega_i dt - fl(omega_i dt)
+  double rc[5][3], rs[5][3];  // per motion type: cos / sin of fl(omega_i dt)
+  double om[5][3];            // per motion type: omega_i
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)
@@ -477,19 +477,20 @@ QT_HD int pattern_omegas(const qt_env_params& e, int motion, double* om) {
   return 0;
 }
 
-inline LaunchConst make_launch_const(const qt_env_params& e, int motion) {
+inline LaunchConst make_launch_const(const qt_env_params& e) {
   LaunchConst k{};
   k.rl = make_rate_lin(e);
   k.pl = make_plant(e, e.mass);
   k.vl = make_vel_lin(e, k.pl);
-  double om[3] = {0.0, 0.0, 0.0};
-  const int na = pattern_omegas(e, motion, om);
-  for (int i = 0; i < na; ++i) {
-    const double a = om[i] * e.dt;
-    k.rc[i] = cos(a);
-    k.rs[i] = sin(a);
-    k.om[i] = om[i];
-    k.ores[i] = fma(om[i], e.dt, -a);  // exact residual of the rounded product
+  for (int m = 0; m < 5; ++m) {
+    double om[3] = {0.0, 0.0, 0.0};
+    const int na = pattern_omegas(e, m, om);
+    for (int i = 0; i < na; ++i) {
+      const double a = om[i] * e.dt;
+      k.rc[m][i] = cos(a);
+      k.rs[m][i] = sin(a);
+      k.om[m][i] = om[i];
+    }
   }
   return k;
 }
@@ -825,6 +826,12 @@ __host__ __device__ constexpr int structured_index(int j) {
   return rows[j] * KC + cols[j];
 }
 
+// a + b * c rounded twice, as numpy evaluates it (no FMA contraction)
+__device__ __forceinline__ double add_product_rn(double a, double b, double c) {
+#pragma clang fp contract(off)
+  return a + b * c;
+}
+
 // RiccatiLQRController.compute_action (riccati_lqr.py:779-967) given the
 // observation the env returned (quad p, v; target p, v, a).  LQI integral
 // update 869-900, output clamps 907-921.  Returns true when saturated.
@@ -879,7 +886,7 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
       // rounded as the reference rounds it (no contraction)
       const double g = em > c.integral_zero_threshold ? c.dt : 0.0;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) integ[i] = __dadd_rn(integ[i], __dmul_rn(g, ep[i]));
+      for (int i = 0; i < 3; ++i) integ[i] = add_product_rn(integ[i], g, ep[i]);
     } else if (em > c.integral_zero_threshold) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -887,9 +894,15 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
         if (!block) integ[i] += c.dt * ep[i];
       }
     }
-    if (lim > 0) {
+    if (FAST) {
+      // the clip to +-lim when lim > 0, else none: a clip to +-inf (the
+      // integral is finite), so no branch in the step loop
+      const double lc = lim > 0 ? lim : INFINITY;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) integ[i] = FAST ? clip_num(integ[i], -lim, lim) : clipd(integ[i], -lim, lim);
+      for (int i = 0; i < 3; ++i) integ[i] = clip_num(integ[i], -lc, lc);
+    } else if (lim > 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i], -lim, lim);
     }
     if (KS) {
       uf[0] = (G.k[0] * s[2] + G.k[1] * s[5]) + G.k[6] * integ[2];

@@ -310,17 +310,20 @@ constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
 // step's bit for bit on the same state, so its on-target and LQI-gate
 // decisions need no knife-edge band.
 __device__ __forceinline__ double sq3_ref(double a, double b, double c) {
-  return __dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c));
+#pragma clang fp contract(off)
+  return (a * a + b * b) + c * c;
 }
 
 // Carried sin / cos of a periodic target's angles (circular: 1, sinusoidal:
 // 3, figure-8: theta = omega t).  Each step rotates them by the launch's
-// fixed rotor (cos, sin)(fl(omega dt)) and then by the first-order
-// correction omega ((t_new - t) - dt) + (omega dt - fl(omega dt)): the
-// carried pair follows sin / cos of omega t_k + phase for the env's
-// accumulated time t_k (t += dt, quadcopter_env.py:191) to a few ulp per
-// step, where the reference evaluates sin / cos of that angle rounded
-// (target_motion.py:86, 144, 179).
+// fixed rotor (cos, sin)(fl(omega dt)) and then to first order by
+// omega ((t_new - t) - dt), the rounding of the env's time step (t += dt,
+// quadcopter_env.py:191; exact by Sterbenz, <= ulp(t)): 7 operations per
+// angle where a sin / cos costs ~30.  They so follow sin / cos of
+// omega t_k + phase for the accumulated t_k, which the reference evaluates
+// rounded (target_motion.py:86, 144, 179), up to the rotor's own rounding
+// (k (omega dt - fl(omega dt)) < 1e-14 rad over 3,000 steps) and a few ulp
+// of drift.
 template <int MOTION>
 struct Rotor {
   static constexpr int NA = MOTION == QT_MOTION_SINUSOIDAL ? 3 : 1;
@@ -343,9 +346,9 @@ __device__ __forceinline__ void rotor_advance(const LaunchConst& k, double dtt, 
 #pragma unroll
   for (int i = 0; i < Rotor<MOTION>::NA; ++i) {
     const double s0 = r.s[i], c0 = r.c[i];
-    const double s1 = fma(s0, k.rc[i], c0 * k.rs[i]);
-    const double c1 = fma(c0, k.rc[i], -(s0 * k.rs[i]));
-    const double d = fma(k.om[i], dtt, k.ores[i]);
+    const double s1 = fma(s0, k.rc[MOTION][i], c0 * k.rs[MOTION][i]);
+    const double c1 = fma(c0, k.rc[MOTION][i], -(s0 * k.rs[MOTION][i]));
+    const double d = k.om[MOTION][i] * dtt;
     r.s[i] = fma(c1, d, s1);
     r.c[i] = fma(-s1, d, c1);
   }
@@ -361,6 +364,41 @@ __device__ __forceinline__ void target_from_rotor(const qt_env_params& e, const 
     for (int i = 0; i < 3; ++i) o.p[i] = e.center[i], o.v[i] = 0.0, o.a[i] = 0.0;
     periodic_state<WANT_ACC>(e, MOTION, pt, r.s, r.c, o);
     if (WANT_ACC) clamp_acceleration(e, o);
+  }
+}
+
+// Runtime-motion form (a wave that straddles two motion groups of a grouped
+// launch): the same per-motion rotor arithmetic as the specialised loops,
+// chosen per lane, so that an episode's results do not depend on the wave it
+// lands in.  `r` holds up to three angles.
+template <bool FF>
+__device__ __forceinline__ void rotor_init_rt(int motion, const Pattern& pt, double t, Rotor<QT_MOTION_SINUSOIDAL>& r) {
+  if (motion == QT_MOTION_SINUSOIDAL)
+    rotor_init<QT_MOTION_SINUSOIDAL>(pt, t, r);
+  else if (motion == QT_MOTION_CIRCULAR)
+    rotor_init<QT_MOTION_CIRCULAR>(pt, t, reinterpret_cast<Rotor<QT_MOTION_CIRCULAR>&>(r));
+  else if (motion == QT_MOTION_FIGURE8 && !FF)
+    rotor_init<QT_MOTION_FIGURE8>(pt, t, reinterpret_cast<Rotor<QT_MOTION_FIGURE8>&>(r));
+}
+
+// ADVANCE: rotate by one step first (dtt: the time step's rounding)
+template <bool FF, bool ADVANCE>
+__device__ __forceinline__ void rotor_target_rt(const qt_env_params& e, const LaunchConst& k, int motion,
+                                                const Pattern& pt, double t, double dtt,
+                                                Rotor<QT_MOTION_SINUSOIDAL>& r, Target& tg) {
+  if (motion == QT_MOTION_SINUSOIDAL) {
+    if (ADVANCE) rotor_advance<QT_MOTION_SINUSOIDAL>(k, dtt, r);
+    target_from_rotor<FF, QT_MOTION_SINUSOIDAL>(e, pt, r, tg);
+  } else if (motion == QT_MOTION_CIRCULAR) {
+    auto& rc = reinterpret_cast<Rotor<QT_MOTION_CIRCULAR>&>(r);
+    if (ADVANCE) rotor_advance<QT_MOTION_CIRCULAR>(k, dtt, rc);
+    target_from_rotor<FF, QT_MOTION_CIRCULAR>(e, pt, rc, tg);
+  } else if (motion == QT_MOTION_FIGURE8 && !FF) {
+    auto& rf = reinterpret_cast<Rotor<QT_MOTION_FIGURE8>&>(r);
+    if (ADVANCE) rotor_advance<QT_MOTION_FIGURE8>(k, dtt, rf);
+    target_from_rotor<false, QT_MOTION_FIGURE8>(e, pt, rf, tg);
+  } else {
+    target_state<FF, true>(e, motion, pt, t, tg);
   }
 }
 
@@ -403,29 +441,34 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   const double R = cr.target_radius, eR = e.target_radius;
   const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
   const int W = cr.overshoot_window;
+  // Launch start: the pre-step tracking error of the current observation,
+  // roll / pitch trig, target rotor, overshoot counter.  The observation is
+  // re-derived from t (the stored one is the same function of t), so that
+  // loop-invariant target rows (a linear target's velocity) stay invariant in
+  // registers.  Nothing is re-derived after a vote stops the loop (the exact
+  // finish changes only velocities and termination codes), so a lane's
+  // results do not depend on the other lanes of its wave.
+  Rotor<kRotor ? MOTION : QT_MOTION_SINUSOIDAL> rot;
+  if constexpr (kRotor) {
+    rotor_init<MOTION>(pt, t, rot);
+    target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+  } else if constexpr (MOTION < 0) {
+    rotor_init_rt<FF>(motion, pt, t, rot);
+    rotor_target_rt<FF, false>(e, k, motion, pt, t, 0.0, rot, tg);
+  } else {
+    target_state<FF, true>(e, motion, pt, t, tg);
+  }
+  double err = sqrt_pos(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
+  Trig ta;
+  trig_of<true>(x + 6, ta);
+  int z = a.prev_on == 1 ? 1 : (a.os_streak >= 0 ? a.os_streak + 1 : kNeg);
+  double cur = a.os_cur;
+  int on_pre = a.on_pre, on_post = a.on_post, os_count = a.os_count;
+  bool stepped = false;
   int s = 0;
   while (a.term == QT_TERM_RUNNING && s < nsteps) {
-    // (re)start: the pre-step tracking error of the current observation,
-    // roll / pitch trig, target rotor, overshoot counter
-    // The observation is re-derived from t (the stored one is the same
-    // function of t), so that loop-invariant target rows (a linear target's
-    // velocity) stay invariant in registers.
-    Rotor<kRotor ? MOTION : QT_MOTION_CIRCULAR> rot;
-    if constexpr (kRotor) {
-      rotor_init<MOTION>(pt, t, rot);
-      target_from_rotor<FF, MOTION>(e, pt, rot, tg);
-    } else {
-      target_state<FF, true>(e, motion, pt, t, tg);
-    }
-    double err = sqrt_pos(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
-    Trig ta;
-    trig_of<true>(x + 6, ta);
-    int z = a.prev_on == 1 ? 1 : (a.os_streak >= 0 ? a.os_streak + 1 : kNeg);
-    double cur = a.os_cur;
-    int on_pre = a.on_pre, on_post = a.on_post, os_count = a.os_count;
     const int s0 = s;
-    const int s_end = nsteps - s0 > (1 << 29) ? s0 + (1 << 29) : nsteps;  // z stays < 1 off phase
-    bool rare = false;
+    int rem = nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0;  // steps left in this run (z stays < 1 off phase)
     do {
       const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_advance)
       // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -461,6 +504,8 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
         if constexpr (kRotor) {
           rotor_advance<MOTION>(k, (t - t0) - e.dt, rot);
           target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+        } else if constexpr (MOTION < 0) {
+          rotor_target_rt<FF, true>(e, k, motion, pt, t, (t - t0) - e.dt, rot, tg);
         } else {
           target_state<FF, true>(e, motion, pt, t, tg);
         }
@@ -475,21 +520,28 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       attitude_trig_advance(x + 6, ap, ta);
       const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
       const bool tl = t >= e.max_episode_time;
-      ++s;
-      // one vote: each compare's lane mask, or-ed on the scalar unit
-      rare = (__builtin_amdgcn_ballot_w64(vbad) | __builtin_amdgcn_ballot_w64(pb) |
-              __builtin_amdgcn_ballot_w64(tl)) != 0;
-    } while (!rare && s < s_end);
-    a.steps += s - s0;
+      --rem;
+      // one vote: each compare's lane mask and the run's end, or-ed on the scalar unit
+      const uint64_t stop = __builtin_amdgcn_ballot_w64(vbad) | __builtin_amdgcn_ballot_w64(pb) |
+                            __builtin_amdgcn_ballot_w64(tl) | (rem == 0 ? ~0ull : 0ull);
+      if (stop) break;
+    } while (true);
+    const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;
+    s += ran;
+    a.steps += ran;
+    stepped = true;
+    z = z <= 0 ? kNeg : z;  // off phase: keep z far below 1 for the next run
+    // finish the last step exactly: the velocity clamp where it acts, per-lane
+    // termination (both no-ops for a lane the vote did not stop)
+    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) clamp_velocity(e, x);
+    a.term = (QT_ABLATE & QT_ABL_TERMINATION) ? (t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING)
+                                               : termination_fast(e, t, x);
+  }
+  if (stepped) {
     a.on_pre = on_pre, a.on_post = on_post, a.os_count = os_count;
     a.prev_on = z == 1 ? 1 : 0;
     a.os_streak = z >= 2 ? z - 1 : -1;
     a.os_cur = cur;
-    if (rare) {  // finish the last step exactly
-      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) clamp_velocity(e, x);
-      a.term = (QT_ABLATE & QT_ABL_TERMINATION) ? (t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING)
-                                                 : termination_fast(e, t, x);
-    }
   }
 }
 
@@ -498,11 +550,10 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // plant constants come from the launch (LaunchConst) and the gains from
 // uniform addresses, all in SGPRs (checked on the host, launch_rollout).
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
-__global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
-                                                         BatchDev b, qt_state st, int nsteps,
-                                                         double* __restrict__ rec, int deferred, LaunchConst lc) {
-  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= b.slot_end) return;
+__device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
+                                             const BatchDev& b, const qt_state& st, int nsteps,
+                                             double* __restrict__ rec, int deferred, const LaunchConst& lc,
+                                             int64_t slot) {
   const int64_t n = b.n, ep = episode_of(b, slot);
   const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
   const Pattern pt = pattern_of(b, e, motion, ep);
@@ -594,6 +645,50 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   store_acc(st.acc, n, ep, a);
 }
 
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
+__global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+                                                         BatchDev b, qt_state st, int nsteps,
+                                                         double* __restrict__ rec, int deferred, LaunchConst lc) {
+  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.slot_end) return;
+  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
+}
+
+// The yaw-at-rest fast flavour over a batch grouped by motion type
+// (qt_rollout_grouped: `order` lists the episodes motion by motion) in ONE
+// launch: each wave runs the loop specialised for its motion; a wave that
+// straddles two groups runs the runtime-motion loop.  One launch keeps every
+// SIMD busy where one launch per group would run each group's waves alone
+// (a 65,536-episode batch of five groups: ~205 waves per launch on 1,024 SIMDs).
+template <int KC, bool FF, bool KS>
+__global__ __launch_bounds__(kBlock) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+                                                                 BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
+  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= b.slot_end) return;
+  const int m = b.motion ? (int)b.motion[episode_of(b, slot)] : e.motion;
+  const int m0 = __builtin_amdgcn_readfirstlane(m);
+  const int wm = __builtin_amdgcn_ballot_w64(m != m0) == 0 ? m0 : -1;
+  switch (wm) {
+    case QT_MOTION_STATIONARY:
+      rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+    case QT_MOTION_LINEAR:
+      rollout_lane<kYaw0, QT_MOTION_LINEAR, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+    case QT_MOTION_CIRCULAR:
+      rollout_lane<kYaw0, QT_MOTION_CIRCULAR, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+    case QT_MOTION_SINUSOIDAL:
+      rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+    case QT_MOTION_FIGURE8:
+      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+    default:
+      rollout_lane<kYaw0, -1, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+  }
+}
+
 inline BatchDev to_dev(const qt_batch* b) {
   return BatchDev{b->n,     b->motion,        b->pattern, b->plant_mass, b->hover_thrust, b->K,
                   b->k_cols, b->k_per_episode, b->order,   0,             b->n};
@@ -610,7 +705,9 @@ inline bool valid_state(const qt_state& st, bool need_integ) {
 // Fast step flavours (qt_rollout_fast.hip): launches rollout_kernel<flavor>
 // (kFast or kYaw0) for the runtime controller / target choice.
 // uni: no per-episode mass, hover thrust or gains (rollout_kernel's UNI).
-void launch_fast(int flavor, bool uni, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
+// grouped: the yaw-at-rest flavour of a motion-grouped batch in one launch
+// (rollout_grouped_kernel; `motion` is ignored).
+void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
                  const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
                  const qt_state& st, int nsteps, const LaunchConst& lc);
 

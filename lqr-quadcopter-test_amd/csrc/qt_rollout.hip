@@ -381,23 +381,30 @@ struct ExactLaunch {
 
 // One rollout launch set: the fast flavour the launch-level preconditions
 // allow, then the exact kernel for the waves it left (or for everything).
+// The step flavour a launch can take (launch-level preconditions).
+int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
+  const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
+  if (fast && (ks || kc == 3 || no_yaw) && rate_bounded_ok(e, c)) return kYaw0;
+  return fast ? kFast : kExact;
+}
+
+// One rollout launch set: the fast flavour the launch-level preconditions
+// allow, then the exact kernel for the waves it left (or for everything).
+// grouped: b covers a motion-grouped batch and the yaw-at-rest flavour runs
+// it in one launch (rollout_grouped_kernel), the exact pass with runtime motion.
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
-                   double* rec) {
-  const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
-  const LaunchConst lc = make_launch_const(e, motion);  // yaw-at-rest closed forms, target rotors
+                   double* rec, bool grouped = false) {
+  const LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
-  int flavor = kExact;
-  if (fast && (ks_eff || no_yaw) && rate_bounded_ok(e, c))
-    flavor = kYaw0;
-  else if (fast)
-    flavor = kFast;
+  const int flavor = flavor_for(kc, ks, no_yaw, e, c, rec);
   if (flavor != kExact) {
-    launch_fast(flavor, uni, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
+    launch_fast(flavor, uni, grouped, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
   }
-  dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, motion, flavor, grid, s, e, c, cr, b, st, nsteps, rec, lc);
+  dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, grouped ? -1 : motion, flavor, grid, s, e, c, cr, b, st, nsteps, rec,
+                                lc);
   return check_launch();
 }
 
@@ -451,6 +458,9 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
   const bool ff = ctrl->feedforward_enabled != 0;
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
+  if (flavor_for(batch->k_cols, ks, no_yaw, *env, *ctrl, rec) == kYaw0)  // every group in one launch
+    return launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, grid_of(batch->n), s, *env, *ctrl, *crit, b, st, nsteps,
+                          rec, true);
   for (int32_t i = 0; i < nseg; ++i) {
     b.slot0 = i ? seg_end[i - 1] : 0;
     b.slot_end = seg_end[i];

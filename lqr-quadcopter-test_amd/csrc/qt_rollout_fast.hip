@@ -43,10 +43,22 @@ struct FastLaunch {
 };
 }  // namespace
 
-void launch_fast(int flavor, bool uni, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
+struct GroupedLaunch {
+  template <int MOTION, int KC, bool FF, bool KS>
+  static void run(int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
+                  const BatchDev& b, const qt_state& st, int nsteps, const LaunchConst& lc) {
+    if constexpr (MOTION == -1)  // one kernel per (KC, FF, KS): instantiated through the runtime-motion slot only
+      rollout_grouped_kernel<KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
+  }
+};
+
+void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
                  const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
                  const qt_state& st, int nsteps, const LaunchConst& lc) {
-  dispatch_rollout<FastLaunch>(kc, ff, ks, motion, flavor, uni, grid, s, e, c, cr, b, st, nsteps, lc);
+  if (grouped && flavor == kYaw0)
+    dispatch_rollout<GroupedLaunch>(kc, ff, ks, -1, grid, s, e, c, cr, b, st, nsteps, lc);
+  else
+    dispatch_rollout<FastLaunch>(kc, ff, ks, motion, flavor, uni, grid, s, e, c, cr, b, st, nsteps, lc);
 }
 
 }  // namespace qtk

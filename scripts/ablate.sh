@@ -9,7 +9,7 @@ for b in ${1:-0 1 2 4 8 16 31}; do
   d=build/abl/$b
   if [ "$mode" = build ]; then
     mkdir -p $d
-    make -s -C lqr-quadcopter-test_amd OBJ=$(pwd)/$d/obj OUT=$(pwd)/$d HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DQT_ABLATE=$b" >/dev/null || exit 1
+    make -s -C lqr-quadcopter-test_amd OBJ=$(pwd)/$d/obj OUT=$(pwd)/$d DEFS="-DQT_ABLATE=$b" >/dev/null || exit 1
   else
     echo "ablate=$b $(QUADTRACK_LIB=$(pwd)/$d/libquadtrack.so timeout -k 10 120 python scripts/perf_sweep.py --n 65536 --motions linear --ctl lqr --reps 3)"
   fi

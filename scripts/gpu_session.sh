@@ -14,6 +14,9 @@ for step in ${STEPS:-tests bench clock sweep}; do
            timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 --motion sinusoidal --ctl lqi > $O/clock_sin_lqi.json 2>> $O/clock.err ;;
     sweep) timeout -k 10 300 python scripts/perf_sweep.py --n 65536 --motions ${MOTIONS:-linear,sinusoidal,circular,figure8,stationary,mixed} \
              --ctl ${CTLS:-lqr,lqi} --reps 3 > $O/sweep.jsonl 2> $O/sweep.err ;;
+    workloads) for cfg in 3 5; do timeout -k 10 300 python scripts/run_workload.py --config $cfg >> $O/workloads.jsonl 2>> $O/workloads.err; done
+               timeout -k 10 300 python scripts/run_workload.py --config 5 --episodes 131072 >> $O/workloads.jsonl 2>> $O/workloads.err
+               timeout -k 10 300 python scripts/run_workload.py --config 4 --episodes 65536 >> $O/workloads.jsonl 2>> $O/workloads.err ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     profile) TAG=${TAG:-run} timeout -k 10 900 scripts/profile_session.sh > $O/profile.log 2>&1 ;;
   esac

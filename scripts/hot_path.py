@@ -54,7 +54,7 @@ def main():
                 spans.append((idx[ins.split()[1]], j))
     inner = [(h, j) for (h, j) in spans
              if not any((h2, j2) != (h, j) and h <= h2 and j2 <= j for (h2, j2) in spans)]
-    loops = [(-sum(len(bl[q]["ins"]) for q in range(h, j + 1)), h) for (h, j) in inner]
+    loops = [(-sum(sum(i.startswith("v_") for i in bl[q]["ins"]) for q in range(h, j + 1)), h) for (h, j) in inner]
     hdrs = [i for i, b in enumerate(bl) if b["hdr"]]
     if "--outer" in sys.argv:
         start = max(hdrs, key=lambda i: len(bl[i]["ins"])) if hdrs else 0

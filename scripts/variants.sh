@@ -9,7 +9,7 @@ for v in ${1:-0 1}; do
   d=build/var/$v
   if [ "$mode" = build ]; then
     mkdir -p $d
-    make -s -C lqr-quadcopter-test_amd OBJ=$(pwd)/$d/obj OUT=$(pwd)/$d HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DQT_VARIANT=$v ${EXTRA_FLAGS:-}" >/dev/null || exit 1
+    make -s -C lqr-quadcopter-test_amd OBJ=$(pwd)/$d/obj OUT=$(pwd)/$d DEFS="-DQT_VARIANT=$v ${EXTRA_FLAGS:-}" >/dev/null || exit 1
   else
     echo "variant=$v $(QUADTRACK_LIB=$(pwd)/$d/libquadtrack.so timeout -k 10 120 python scripts/perf_sweep.py --n 65536 --motions ${MOTIONS:-linear} --ctl ${CTLS:-lqr} --reps 5)" || exit 1
   fi
