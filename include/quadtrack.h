@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 2
+#define QT_ABI_VERSION 3
 
 /* error codes */
 #define QT_OK 0
@@ -157,6 +157,14 @@ typedef struct qt_batch {
                                    it): yaw never moves from rest and the yaw-at-rest fast
                                    flavour applies to dense gains too */
   const int32_t* order;         /* [n] or NULL */
+  const double* ff;             /* ABI 3: [7][n] per-episode feed-forward, or NULL (then the qt_ctrl_params
+                                   feed-forward applies to every episode): rows velocity gain xyz,
+                                   acceleration gain xyz, target-velocity clamp (riccati_lqr.py:836-861,
+                                   controllers/__init__.py:286-330).  An episode without feed-forward has
+                                   gains 0 and clamp +inf: the tuner's per-candidate feed-forward gain
+                                   ranges (controllers/tuning.py:689-735) and the heuristic fallback of a
+                                   failed DARE, which runs without it (riccati_lqr.py:764-776).  The
+                                   acceleration clamp stays qt_ctrl_params.ff_max_acceleration. */
 } qt_batch;
 
 /* Mutable per-episode rollout state, all [.][n] SoA device arrays. */
@@ -207,11 +215,14 @@ int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo
 int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, void* stream);
 
-/* qt_rollout for a batch of mixed motion types, one motion-specialised launch
-   per group (no per-step motion dispatch).  batch->order must list the episodes
-   grouped by motion: slots [seg_end[i-1], seg_end[i]) (seg_end[-1] = 0) all
-   have motion seg_motion[i]; seg_end[nseg-1] == n.  seg_motion and seg_end are
-   HOST arrays.  Results are identical to qt_rollout's. */
+/* qt_rollout for a batch of mixed motion types without per-step motion
+   dispatch.  batch->order must list the episodes grouped by motion: slots
+   [seg_end[i-1], seg_end[i]) (seg_end[-1] = 0) all have motion seg_motion[i];
+   seg_end[nseg-1] == n.  seg_motion and seg_end are HOST arrays.  The
+   yaw-at-rest fast flavour runs every group in ONE launch (each 64-lane wave
+   takes the loop specialised for its motion; the <= nseg-1 waves that straddle
+   two groups take the runtime-motion loop, same per-lane arithmetic); other
+   flavours launch once per group.  Results are identical to qt_rollout's. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);

@@ -79,31 +79,38 @@ struct Target {
 };
 
 // Position / velocity / acceleration of a periodic pattern from the sin / cos
-// of its angles (circular target_motion.py:84-100, sinusoidal 142-153); the
-// caller has set o to the centre and zeros.
+// of its angles (circular target_motion.py:84-100, sinusoidal 142-153).
+// Every branch forms all nine components as values and o is written once at
+// the end: stores of different fields in the two branches would otherwise be
+// sunk into one store through a pointer phi, which keeps the Target in
+// scratch memory.
 template <bool WANT_ACC>
 __device__ __forceinline__ void periodic_state(const qt_env_params& e, int motion, const Pattern& pt,
                                                const double* s, const double* c, Target& o) {
+  double p[3], v[3], a[3];
   if (motion == QT_MOTION_CIRCULAR) {
     const double r = e.radius, om = pt.c1;
-    o.p[0] = e.center[0] + r * c[0];
-    o.p[1] = e.center[1] + r * s[0];
-    o.v[0] = -r * om * s[0];
-    o.v[1] = r * om * c[0];
-    if (WANT_ACC) {
-      o.a[0] = -r * (om * om) * c[0];
-      o.a[1] = -r * (om * om) * s[0];
-    }
+    p[0] = e.center[0] + r * c[0];
+    p[1] = e.center[1] + r * s[0];
+    p[2] = e.center[2];
+    v[0] = -r * om * s[0];
+    v[1] = r * om * c[0];
+    v[2] = 0.0;
+    a[0] = WANT_ACC ? -r * (om * om) * c[0] : 0.0;
+    a[1] = WANT_ACC ? -r * (om * om) * s[0] : 0.0;
+    a[2] = 0.0;
   } else {
     const double amp[3] = {e.amplitude, e.amplitude * 0.5, e.amplitude * 0.25};
     const double om[3] = {pt.o0, pt.o1, pt.o2};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      o.p[i] = e.center[i] + amp[i] * s[i];
-      o.v[i] = amp[i] * om[i] * c[i];
-      if (WANT_ACC) o.a[i] = -amp[i] * (om[i] * om[i]) * s[i];
+      p[i] = e.center[i] + amp[i] * s[i];
+      v[i] = amp[i] * om[i] * c[i];
+      a[i] = WANT_ACC ? -amp[i] * (om[i] * om[i]) * s[i] : 0.0;
     }
   }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o.p[i] = p[i], o.v[i] = v[i], o.a[i] = a[i];
 }
 
 // TargetMotion.get_state's acceleration clamp (target_motion.py:403-405).
@@ -158,11 +165,6 @@ __device__ __forceinline__ void figure8_recip(const qt_env_params& e, double om,
 template <bool WANT_ACC, bool RECIP = false>
 __device__ __forceinline__ void target_state(const qt_env_params& e, int motion, const Pattern& pt, double t,
                                              Target& o) {
-  o.p[0] = e.center[0];
-  o.p[1] = e.center[1];
-  o.p[2] = e.center[2];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) o.v[i] = 0.0, o.a[i] = 0.0;
   if (motion == QT_MOTION_LINEAR) {
     o.p[0] = e.center[0] + pt.c0 * t;
     o.p[1] = e.center[1] + pt.c1 * t;
@@ -170,10 +172,13 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     o.v[0] = pt.c0;
     o.v[1] = pt.c1;
     o.v[2] = pt.c2;
+    o.a[0] = o.a[1] = o.a[2] = 0.0;
   } else if (motion == QT_MOTION_CIRCULAR || motion == QT_MOTION_SINUSOIDAL) {
     double th[3], s[3], c[3];
     const int na = periodic_angles(motion, pt, t, th);
-    for (int i = 0; i < na; ++i) fast_sincos(th[i], &s[i], &c[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)  // compile-time indices: the arrays stay in registers
+      if (i < na) fast_sincos(th[i], &s[i], &c[i]);
     periodic_state<WANT_ACC>(e, motion, pt, s, c, o);
   } else if (motion == QT_MOTION_FIGURE8 && RECIP && !WANT_ACC) {
     double st, ct;
@@ -187,10 +192,11 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     double dcos = -st * om, dsin = ct * om;
     double dden = 2.0 * st * dsin;
     double den2 = den * den;
-    o.p[0] = e.center[0] + sc * ct / den;
-    o.p[1] = e.center[1] + sc * st * ct / den;
-    o.v[0] = sc * ((dcos * den - ct * dden) / den2);
-    o.v[1] = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
+    const double p0 = e.center[0] + sc * ct / den;
+    const double p1 = e.center[1] + sc * st * ct / den;
+    const double v0 = sc * ((dcos * den - ct * dden) / den2);
+    const double v1 = sc * (((dsin * ct + st * dcos) * den - st * ct * dden) / den2);
+    double a0 = 0.0, a1 = 0.0;
     if (WANT_ACC) {
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;
@@ -199,10 +205,16 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
       double denp = 1.0 + stp * stp;
       double pp0 = e.center[0] + sc * ctp / denp;
       double pp1 = e.center[1] + sc * stp * ctp / denp;
-      o.a[0] = ((pp0 - o.p[0]) / h - o.v[0]) / h;
-      o.a[1] = ((pp1 - o.p[1]) / h - o.v[1]) / h;
-      o.a[2] = 0.0;
+      a0 = ((pp0 - p0) / h - v0) / h;
+      a1 = ((pp1 - p1) / h - v1) / h;
     }
+    o.p[0] = p0, o.p[1] = p1, o.p[2] = e.center[2];
+    o.v[0] = v0, o.v[1] = v1, o.v[2] = 0.0;
+    o.a[0] = a0, o.a[1] = a1, o.a[2] = 0.0;
+  } else {  // stationary
+    o.p[0] = e.center[0], o.p[1] = e.center[1], o.p[2] = e.center[2];
+    o.v[0] = o.v[1] = o.v[2] = 0.0;
+    o.a[0] = o.a[1] = o.a[2] = 0.0;
   }
   if (WANT_ACC) clamp_acceleration(e, o);
 }
@@ -259,8 +271,6 @@ __device__ __forceinline__ void target_state_carried(const qt_env_params& e, con
 #pragma unroll
     for (int i = 0; i < NA; ++i) fast_sincos(th[i], &r.s[i], &r.c[i]);
   }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) o.p[i] = e.center[i], o.v[i] = 0.0, o.a[i] = 0.0;
   periodic_state<WANT_ACC>(e, MOTION, pt, r.s, r.c, o);
   if (WANT_ACC) clamp_acceleration(e, o);
 }
@@ -826,6 +836,26 @@ __host__ __device__ constexpr int structured_index(int j) {
   return rows[j] * KC + cols[j];
 }
 
+// Feed-forward parameters of one episode (riccati_lqr.py:836-861,
+// controllers/__init__.py:286-330): velocity / acceleration gains and the
+// velocity clamp.  Feed-forward off is the identity with these parameters:
+// zero gains and no clamp give the reference's plain v_T - v and zero
+// acceleration terms (up to the sign of a zero, which no later operation
+// distinguishes), so one code path serves lanes with and without it — the
+// per-episode form of qt_batch.ff (the tuner's feed-forward gain ranges; the
+// heuristic fallback of a failed DARE, which runs without feed-forward,
+// riccati_lqr.py:764-776).
+struct FFLane {
+  double vg[3], ag[3], vmax;
+};
+
+__host__ __device__ inline FFLane ff_uniform(const qt_ctrl_params& c) {
+  if (!c.feedforward_enabled) return FFLane{{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, INFINITY};
+  return FFLane{{c.ff_velocity_gain[0], c.ff_velocity_gain[1], c.ff_velocity_gain[2]},
+                {c.ff_acceleration_gain[0], c.ff_acceleration_gain[1], c.ff_acceleration_gain[2]},
+                c.ff_max_velocity};
+}
+
 // a + b * c rounded twice, as numpy evaluates it (no FMA contraction)
 __device__ __forceinline__ double add_product_rn(double a, double b, double c) {
 #pragma clang fp contract(off)
@@ -837,25 +867,27 @@ __device__ __forceinline__ double add_product_rn(double a, double b, double c) {
 // update 869-900, output clamps 907-921.  Returns true when saturated.
 // FAST: gains, hover thrust and observation are known finite, so the raw
 // command is finite and np.clip's NaN pass-through cannot arise.
+// FF: the feed-forward arithmetic is compiled in (some lane may have it on);
+// its parameters are the lane's, `f` (ff_uniform / qt_batch.ff).
 template <int KC, bool FF, bool KS, bool FAST = false>
 __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Gains<KC, KS>& G, double hover,
                                                const double* qp, const double* qv, const Target& tg,
-                                               double* integ, double* u, double* diag = nullptr,
+                                               const FFLane& f, double* integ, double* u, double* diag = nullptr,
                                                double em_fast = 0.0) {
   double ep[3], ev[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 3; ++i) ep[i] = tg.p[i] - qp[i];
-  if (FF && c.feedforward_enabled) {
+  if (FF) {
     double vm = norm3(tv[0], tv[1], tv[2]);
-    if (vm > c.ff_max_velocity) {
-      double scl = c.ff_max_velocity / vm;
+    if (vm > f.vmax) {
+      double scl = f.vmax / vm;
 #pragma unroll
       for (int i = 0; i < 3; ++i) tv[i] = tv[i] * scl;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      ffv[i] = c.ff_velocity_gain[i] * tv[i];  // diagnostics term (riccati_lqr.py:851)
-      tv[i] = (1.0 + c.ff_velocity_gain[i]) * tv[i];
+      ffv[i] = f.vg[i] * tv[i];  // diagnostics term (riccati_lqr.py:851)
+      tv[i] = (1.0 + f.vg[i]) * tv[i];
     }
     double ac[3] = {tg.a[0], tg.a[1], tg.a[2]};
     double am = norm3(ac[0], ac[1], ac[2]);
@@ -864,7 +896,7 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
       for (int i = 0; i < 3; ++i) ac[i] = ac[i] / am * c.ff_max_acceleration;
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) ffa[i] = c.ff_acceleration_gain[i] * ac[i];
+    for (int i = 0; i < 3; ++i) ffa[i] = f.ag[i] * ac[i];
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i) ev[i] = tv[i] - qv[i];
@@ -975,8 +1007,8 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
 template <bool FF, bool FAST = false>
 __device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, const double* g, double hover,
                                                    const double* qp, const double* qv, const Target& tg, double now,
-                                                   double* integ, double* u, double* diag = nullptr,
-                                               double em_fast = 0.0) {
+                                                   const FFLane& f, double* integ, double* u,
+                                                   double* diag = nullptr) {
   const double *kp = g, *ki = g + 3, *kd = g + 6;
   double ep[3], tv[3] = {tg.v[0], tg.v[1], tg.v[2]}, ffa[3] = {0, 0, 0}, ffv[3] = {0, 0, 0};
 #pragma unroll
@@ -999,17 +1031,17 @@ __device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, cons
 #pragma unroll
     for (int i = 0; i < 3; ++i) integ[i] = clipd(integ[i] + ep[i] * dt, -lim, lim);
   }
-  if (FF && c.feedforward_enabled) {
+  if (FF) {
     const double vm = norm3(tv[0], tv[1], tv[2]);
-    if (vm > c.ff_max_velocity && vm > 0) {
-      const double scl = c.ff_max_velocity / vm;
+    if (vm > f.vmax && vm > 0) {
+      const double scl = f.vmax / vm;
 #pragma unroll
       for (int i = 0; i < 3; ++i) tv[i] = tv[i] * scl;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      tv[i] = (1.0 + c.ff_velocity_gain[i]) * tv[i];
-      ffv[i] = kd[i] * c.ff_velocity_gain[i] * tv[i] / (1.0 + c.ff_velocity_gain[i]);
+      tv[i] = (1.0 + f.vg[i]) * tv[i];
+      ffv[i] = kd[i] * f.vg[i] * tv[i] / (1.0 + f.vg[i]);
     }
     double ac[3] = {tg.a[0], tg.a[1], tg.a[2]};
     const double am = norm3(ac[0], ac[1], ac[2]);
@@ -1018,7 +1050,7 @@ __device__ __forceinline__ void compute_action_pid(const qt_ctrl_params& c, cons
       for (int i = 0; i < 3; ++i) ac[i] = ac[i] / am * c.ff_max_acceleration;
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) ffa[i] = c.ff_acceleration_gain[i] * ac[i];
+    for (int i = 0; i < 3; ++i) ffa[i] = f.ag[i] * ac[i];
   }
   double p[3], it[3], d[3], corr[3];
 #pragma unroll

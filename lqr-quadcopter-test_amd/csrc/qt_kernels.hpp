@@ -92,8 +92,25 @@ struct BatchDev {
   int32_t k_cols;
   int32_t k_per_episode;
   const int32_t* order;
+  const double* ff;         // [7][n] per-episode feed-forward (qt_batch.ff) or NULL
   int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
 };
+
+// The slot a launch position runs, or -1 past the launch's slot range.
+__device__ __forceinline__ int64_t slot_at(const BatchDev& b, int64_t p) {
+  const int64_t slot = b.slot0 + p;
+  return slot < b.slot_end ? slot : -1;
+}
+
+// The lane's feed-forward parameters: per episode (qt_batch.ff rows: velocity
+// gain xyz, acceleration gain xyz, velocity clamp) or the controller's.
+__device__ __forceinline__ FFLane ff_of(const BatchDev& b, const qt_ctrl_params& c, int64_t ep) {
+  if (!b.ff) return ff_uniform(c);
+  const int64_t n = b.n;
+  return FFLane{{b.ff[0 * n + ep], b.ff[1 * n + ep], b.ff[2 * n + ep]},
+                {b.ff[3 * n + ep], b.ff[4 * n + ep], b.ff[5 * n + ep]},
+                b.ff[6 * n + ep]};
+}
 
 __device__ __forceinline__ int64_t episode_of(const BatchDev& b, int64_t slot) {
   return b.order ? (int64_t)b.order[slot] : slot;
@@ -156,9 +173,9 @@ __device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int
 template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
 __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
-                                          const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
-                                          Acc& a, int nsteps, double* __restrict__ rec, int64_t n, int64_t ep,
-                                          const RateLin& rl) {
+                                          const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
+                                          Target& tg, double& t, Acc& a, int nsteps, double* __restrict__ rec,
+                                          int64_t n, int64_t ep, const RateLin& rl) {
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
@@ -193,9 +210,9 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       u[0] = hover, u[1] = u[2] = u[3] = 0.0;
     } else {
       if constexpr (KC == 3)
-        compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
+        compute_action_pid<FF, FAST>(c, G.k, hover, x, x + 3, tg, t, fl, integ, u);  // observation time = t
       else
-        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err_fast);
+        compute_action<KC, FF, KS, FAST>(c, G, hover, x, x + 3, tg, fl, integ, u, nullptr, err_fast);
     }
     // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics accumulators
     if (!(QT_ABLATE & QT_ABL_METRICS)) {
@@ -327,76 +344,71 @@ __device__ __forceinline__ double sq3_ref(double a, double b, double c) {
 template <int MOTION>
 struct Rotor {
   static constexpr int NA = MOTION == QT_MOTION_SINUSOIDAL ? 3 : 1;
-  double s[NA], c[NA];
+  double s[3], c[3];  // the first NA used
 };
 
 template <int MOTION>
-__device__ __forceinline__ void rotor_init(const Pattern& pt, double t, Rotor<MOTION>& r) {
+__device__ __forceinline__ void rotor_init(const Pattern& pt, double t, double* rs, double* rc) {
   double th[3];
   if (MOTION == QT_MOTION_FIGURE8)
     th[0] = pt.o0 * t;
   else
     periodic_angles(MOTION, pt, t, th);
 #pragma unroll
-  for (int i = 0; i < Rotor<MOTION>::NA; ++i) fast_sincos(th[i], &r.s[i], &r.c[i]);
+  for (int i = 0; i < Rotor<MOTION>::NA; ++i) fast_sincos(th[i], &rs[i], &rc[i]);
 }
 
 template <int MOTION>
-__device__ __forceinline__ void rotor_advance(const LaunchConst& k, double dtt, Rotor<MOTION>& r) {
+__device__ __forceinline__ void rotor_advance(const LaunchConst& k, double dtt, double* rs, double* rc) {
 #pragma unroll
   for (int i = 0; i < Rotor<MOTION>::NA; ++i) {
-    const double s0 = r.s[i], c0 = r.c[i];
+    const double s0 = rs[i], c0 = rc[i];
     const double s1 = fma(s0, k.rc[MOTION][i], c0 * k.rs[MOTION][i]);
     const double c1 = fma(c0, k.rc[MOTION][i], -(s0 * k.rs[MOTION][i]));
     const double d = k.om[MOTION][i] * dtt;
-    r.s[i] = fma(c1, d, s1);
-    r.c[i] = fma(-s1, d, c1);
+    rs[i] = fma(c1, d, s1);
+    rc[i] = fma(-s1, d, c1);
   }
 }
 
 template <bool WANT_ACC, int MOTION>
-__device__ __forceinline__ void target_from_rotor(const qt_env_params& e, const Pattern& pt, const Rotor<MOTION>& r,
-                                                  Target& o) {
+__device__ __forceinline__ void target_from_rotor(const qt_env_params& e, const Pattern& pt, const double* rs,
+                                                  const double* rc, Target& o) {
   if constexpr (MOTION == QT_MOTION_FIGURE8) {
-    figure8_recip(e, pt.o0, r.s[0], r.c[0], o);  // no feed-forward: no acceleration
+    figure8_recip(e, pt.o0, rs[0], rc[0], o);  // no feed-forward: no acceleration
   } else {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) o.p[i] = e.center[i], o.v[i] = 0.0, o.a[i] = 0.0;
-    periodic_state<WANT_ACC>(e, MOTION, pt, r.s, r.c, o);
+    periodic_state<WANT_ACC>(e, MOTION, pt, rs, rc, o);
     if (WANT_ACC) clamp_acceleration(e, o);
   }
 }
 
-// Runtime-motion form (a wave that straddles two motion groups of a grouped
-// launch): the same per-motion rotor arithmetic as the specialised loops,
-// chosen per lane, so that an episode's results do not depend on the wave it
-// lands in.  `r` holds up to three angles.
+// Runtime-motion form (a wave whose lanes have different motion types): the
+// same per-motion rotor arithmetic as the specialised loops, chosen per lane,
+// so that an episode's results do not depend on the wave it lands in.
 template <bool FF>
-__device__ __forceinline__ void rotor_init_rt(int motion, const Pattern& pt, double t, Rotor<QT_MOTION_SINUSOIDAL>& r) {
+__device__ __forceinline__ void rotor_init_rt(int motion, const Pattern& pt, double t, double* rs, double* rc) {
   if (motion == QT_MOTION_SINUSOIDAL)
-    rotor_init<QT_MOTION_SINUSOIDAL>(pt, t, r);
+    rotor_init<QT_MOTION_SINUSOIDAL>(pt, t, rs, rc);
   else if (motion == QT_MOTION_CIRCULAR)
-    rotor_init<QT_MOTION_CIRCULAR>(pt, t, reinterpret_cast<Rotor<QT_MOTION_CIRCULAR>&>(r));
+    rotor_init<QT_MOTION_CIRCULAR>(pt, t, rs, rc);
   else if (motion == QT_MOTION_FIGURE8 && !FF)
-    rotor_init<QT_MOTION_FIGURE8>(pt, t, reinterpret_cast<Rotor<QT_MOTION_FIGURE8>&>(r));
+    rotor_init<QT_MOTION_FIGURE8>(pt, t, rs, rc);
 }
 
 // ADVANCE: rotate by one step first (dtt: the time step's rounding)
 template <bool FF, bool ADVANCE>
 __device__ __forceinline__ void rotor_target_rt(const qt_env_params& e, const LaunchConst& k, int motion,
-                                                const Pattern& pt, double t, double dtt,
-                                                Rotor<QT_MOTION_SINUSOIDAL>& r, Target& tg) {
+                                                const Pattern& pt, double t, double dtt, double* rs, double* rc,
+                                                Target& tg) {
   if (motion == QT_MOTION_SINUSOIDAL) {
-    if (ADVANCE) rotor_advance<QT_MOTION_SINUSOIDAL>(k, dtt, r);
-    target_from_rotor<FF, QT_MOTION_SINUSOIDAL>(e, pt, r, tg);
+    if (ADVANCE) rotor_advance<QT_MOTION_SINUSOIDAL>(k, dtt, rs, rc);
+    target_from_rotor<FF, QT_MOTION_SINUSOIDAL>(e, pt, rs, rc, tg);
   } else if (motion == QT_MOTION_CIRCULAR) {
-    auto& rc = reinterpret_cast<Rotor<QT_MOTION_CIRCULAR>&>(r);
-    if (ADVANCE) rotor_advance<QT_MOTION_CIRCULAR>(k, dtt, rc);
-    target_from_rotor<FF, QT_MOTION_CIRCULAR>(e, pt, rc, tg);
+    if (ADVANCE) rotor_advance<QT_MOTION_CIRCULAR>(k, dtt, rs, rc);
+    target_from_rotor<FF, QT_MOTION_CIRCULAR>(e, pt, rs, rc, tg);
   } else if (motion == QT_MOTION_FIGURE8 && !FF) {
-    auto& rf = reinterpret_cast<Rotor<QT_MOTION_FIGURE8>&>(r);
-    if (ADVANCE) rotor_advance<QT_MOTION_FIGURE8>(k, dtt, rf);
-    target_from_rotor<false, QT_MOTION_FIGURE8>(e, pt, rf, tg);
+    if (ADVANCE) rotor_advance<QT_MOTION_FIGURE8>(k, dtt, rs, rc);
+    target_from_rotor<false, QT_MOTION_FIGURE8>(e, pt, rs, rc, tg);
   } else {
     target_state<FF, true>(e, motion, pt, t, tg);
   }
@@ -431,8 +443,8 @@ __device__ __forceinline__ void clamp_velocity(const qt_env_params& e, double* x
 template <int MOTION, int KC, bool FF, bool KS, bool UNI>
 __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                          int motion, const Pattern& pt, const Plant& pl_lane, double hover,
-                                         const Gains<KC, KS>& G, double* x, double* integ, Target& tg, double& t,
-                                         Acc& a, int nsteps, const LaunchConst& k) {
+                                         const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
+                                         Target& tg, double& t, Acc& a, int nsteps, const LaunchConst& k) {
   constexpr bool kRotor = MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
                           (MOTION == QT_MOTION_FIGURE8 && !FF);
   constexpr int kNeg = -(1 << 30);
@@ -448,13 +460,13 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   // registers.  Nothing is re-derived after a vote stops the loop (the exact
   // finish changes only velocities and termination codes), so a lane's
   // results do not depend on the other lanes of its wave.
-  Rotor<kRotor ? MOTION : QT_MOTION_SINUSOIDAL> rot;
+  double rs[3] = {0.0, 0.0, 0.0}, rc[3] = {1.0, 1.0, 1.0};  // carried target rotor (Rotor)
   if constexpr (kRotor) {
-    rotor_init<MOTION>(pt, t, rot);
-    target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+    rotor_init<MOTION>(pt, t, rs, rc);
+    target_from_rotor<FF, MOTION>(e, pt, rs, rc, tg);
   } else if constexpr (MOTION < 0) {
-    rotor_init_rt<FF>(motion, pt, t, rot);
-    rotor_target_rt<FF, false>(e, k, motion, pt, t, 0.0, rot, tg);
+    rotor_init_rt<FF>(motion, pt, t, rs, rc);
+    rotor_target_rt<FF, false>(e, k, motion, pt, t, 0.0, rs, rc, tg);
   } else {
     target_state<FF, true>(e, motion, pt, t, tg);
   }
@@ -477,9 +489,9 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
         u[0] = hover, u[1] = u[2] = u[3] = 0.0;
       } else {
         if constexpr (KC == 3)
-          compute_action_pid<FF, true>(c, G.k, hover, x, x + 3, tg, t, integ, u);  // observation time = t
+          compute_action_pid<FF, true>(c, G.k, hover, x, x + 3, tg, t, fl, integ, u);  // observation time = t
         else
-          compute_action<KC, FF, KS, true>(c, G, hover, x, x + 3, tg, integ, u, nullptr, err);
+          compute_action<KC, FF, KS, true>(c, G, hover, x, x + 3, tg, fl, integ, u, nullptr, err);
       }
       // ---- the Evaluator's pre-step record (eval.py:142-159) -> metrics
       if (!(QT_ABLATE & QT_ABL_METRICS)) {
@@ -502,10 +514,10 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kRotor) {
-          rotor_advance<MOTION>(k, (t - t0) - e.dt, rot);
-          target_from_rotor<FF, MOTION>(e, pt, rot, tg);
+          rotor_advance<MOTION>(k, (t - t0) - e.dt, rs, rc);
+          target_from_rotor<FF, MOTION>(e, pt, rs, rc, tg);
         } else if constexpr (MOTION < 0) {
-          rotor_target_rt<FF, true>(e, k, motion, pt, t, (t - t0) - e.dt, rot, tg);
+          rotor_target_rt<FF, true>(e, k, motion, pt, t, (t - t0) - e.dt, rs, rc, tg);
         } else {
           target_state<FF, true>(e, motion, pt, t, tg);
         }
@@ -561,6 +573,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   const double hover = UNI ? c.hover_thrust : (b.hover ? b.hover[ep] : c.hover_thrust);
   Gains<KC, KS> G;
   load_gains<KC, KS, UNI>(b, ep, G);
+  const FFLane fl = FF ? ff_of(b, c, ep) : FFLane{};
 
   // integ: LQI integral (KC 9) | PID integral error + last observation time (KC 3)
   constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
@@ -588,6 +601,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   bool lane_ok = a.term != QT_TERM_RUNNING ||
                  (all_finite(G.k, Gains<KC, KS>::kCount) && all_finite(x, 12) && all_finite(integ, 3) &&
                   all_finite(tg.p, 3) && all_finite(tg.v, 3) && all_finite(tg.a, 3) && finite_bits(hover) &&
+                  (!FF || (all_finite(fl.vg, 3) && all_finite(fl.ag, 3) && !(fl.vmax < 0.0))) &&
                   finite_bits(pl.inv_mass) && finite_bits(t) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
   // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
@@ -604,13 +618,13 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     if constexpr (FLAVOR == kYaw0)
-      run_yaw0<MOTION, KC, FF, KS, UNI>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, lc);
+      run_yaw0<MOTION, KC, FF, KS, UNI>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, lc);
     else
-      run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps,
+      run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
                                                  rec, n, ep, lc.rl);
 #if QT_CLOCK_STAMP && defined(QT_FAST_TU)
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    const int64_t wave = (slot - b.slot0) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     if ((threadIdx.x & 63) == 0 && wave < kStampWaves) {
       g_qt_stamps[wave][0] = t0, g_qt_stamps[wave][1] = t1;
       g_qt_stamps[wave][2] = r0, g_qt_stamps[wave][3] = r1;
@@ -618,8 +632,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
 #endif
   } else {
     if (deferred != kExact && wave_ok) return;
-    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, x, integ, tg, t, a, nsteps, rec,
-                                                n, ep, lc.rl);
+    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
+                                                rec, n, ep, lc.rl);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
   // feed-forward reads them); the stored observation carries the reference's
@@ -649,22 +663,25 @@ template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
-  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= b.slot_end) return;
+  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
+  if (slot < 0) return;
   rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
 }
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type
 // (qt_rollout_grouped: `order` lists the episodes motion by motion) in ONE
 // launch: each wave runs the loop specialised for its motion; a wave that
-// straddles two groups runs the runtime-motion loop.  One launch keeps every
-// SIMD busy where one launch per group would run each group's waves alone
-// (a 65,536-episode batch of five groups: ~205 waves per launch on 1,024 SIMDs).
+// straddles two groups (at most one per group boundary) runs the
+// runtime-motion loop, whose target arithmetic per lane is the specialised
+// loops' own (rotor_target_rt), so results do not depend on the wave.  One
+// launch keeps every SIMD busy where one launch per group would run each
+// group's waves alone (65,536 episodes of five groups: ~205 waves per launch
+// on 1,024 SIMDs), and wave count stays ceil(n / 64).
 template <int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                                  BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
-  const int64_t slot = b.slot0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= b.slot_end) return;
+  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
+  if (slot < 0) return;
   const int m = b.motion ? (int)b.motion[episode_of(b, slot)] : e.motion;
   const int m0 = __builtin_amdgcn_readfirstlane(m);
   const int wm = __builtin_amdgcn_ballot_w64(m != m0) == 0 ? m0 : -1;
@@ -690,8 +707,11 @@ __global__ __launch_bounds__(kBlock) void rollout_grouped_kernel(qt_env_params e
 }
 
 inline BatchDev to_dev(const qt_batch* b) {
-  return BatchDev{b->n,     b->motion,        b->pattern, b->plant_mass, b->hover_thrust, b->K,
-                  b->k_cols, b->k_per_episode, b->order,   0,             b->n};
+  BatchDev d{};
+  d.n = b->n, d.motion = b->motion, d.pattern = b->pattern, d.plant_mass = b->plant_mass;
+  d.hover = b->hover_thrust, d.K = b->K, d.k_cols = b->k_cols, d.k_per_episode = b->k_per_episode;
+  d.order = b->order, d.ff = b->ff, d.slot0 = 0, d.slot_end = b->n;
+  return d;
 }
 
 inline int grid_of(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }

@@ -120,9 +120,9 @@ __global__ __launch_bounds__(kBlock) void action_kernel(qt_ctrl_params c, BatchD
   double dg[ND];
   bool sat = false;
   if constexpr (KC == 3)
-    compute_action_pid<true>(c, G.k, hover, qp, qv, tg, obs[15 * n + ep], in, u, dg);  // row 15: time
+    compute_action_pid<true>(c, G.k, hover, qp, qv, tg, obs[15 * n + ep], ff_of(b, c, ep), in, u, dg);  // row 15: time
   else
-    sat = compute_action<KC, true, false>(c, G, hover, qp, qv, tg, in, u, dg);
+    sat = compute_action<KC, true, false>(c, G, hover, qp, qv, tg, ff_of(b, c, ep), in, u, dg);
 #pragma unroll
   for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
   if (diag) {
@@ -433,7 +433,7 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   const int grid = grid_of(batch->n);
   const int motion = batch->motion ? -1 : env->motion;
   hipStream_t s = (hipStream_t)stream;
-  const bool ff = ctrl->feedforward_enabled != 0;
+  const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
   return launch_rollout(batch->k_cols, ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
@@ -455,7 +455,7 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
   if (batch->n == 0 || nsteps == 0) return QT_OK;
   BatchDev b = to_dev(batch);
   hipStream_t s = (hipStream_t)stream;
-  const bool ff = ctrl->feedforward_enabled != 0;
+  const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
   if (flavor_for(batch->k_cols, ks, no_yaw, *env, *ctrl, rec) == kYaw0)  // every group in one launch

@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
 LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # enums (include/quadtrack.h)
 MOTIONS = ("stationary", "linear", "circular", "sinusoidal", "figure8")
@@ -69,7 +69,7 @@ class Batch(C.Structure):
     _fields_ = [("n", C.c_int64), ("motion", C.c_void_p), ("pattern", C.c_void_p), ("plant_mass", C.c_void_p),
                 ("hover_thrust", C.c_void_p), ("K", C.c_void_p), ("k_cols", C.c_int32),
                 ("k_per_episode", C.c_int32), ("k_structured", C.c_int32), ("k_no_yaw", C.c_int32),
-                ("order", C.c_void_p)]
+                ("order", C.c_void_p), ("ff", C.c_void_p)]
 
 
 class State(C.Structure):

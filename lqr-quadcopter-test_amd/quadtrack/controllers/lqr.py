@@ -91,7 +91,7 @@ class BatchedLQR:
     use_lqi = False
 
     def __init__(self, config: dict | None = None, device=None, *, q_pos=None, q_vel=None, r_thrust=None,
-                 r_rate=None, K=None, mass=None):
+                 r_rate=None, K=None, mass=None, ff_velocity_gain=None, ff_acceleration_gain=None):
         config = dict(config or {})
         self.config = config
         self.device = _abi.require_gpu(device)
@@ -100,7 +100,8 @@ class BatchedLQR:
         if isinstance(mass, torch.Tensor):
             mass = mass.detach().to("cpu", torch.float64).numpy()
         given = {k: v for k, v in (("q_pos", q_pos), ("q_vel", q_vel), ("r_thrust", r_thrust), ("r_rate", r_rate),
-                                   ("K", K), ("mass", mass)) if v is not None}
+                                   ("K", K), ("mass", mass), ("ff_velocity_gain", ff_velocity_gain),
+                                   ("ff_acceleration_gain", ff_acceleration_gain)) if v is not None}
         lens = {len(v) for v in given.values()}
         if len(lens) > 1:
             raise ValueError(f"per-episode arrays disagree on the episode count: {sorted(lens)}")
@@ -133,6 +134,14 @@ class BatchedLQR:
                                 config.get("ff_acceleration_gain", [0.0, 0.0, 0.0]),
                                 config.get("ff_max_velocity", 10.0), config.get("ff_max_acceleration", 5.0))
         self.status = torch.zeros(m, dtype=torch.int8, device=self.device)
+        # per-episode feed-forward gains (qt_batch.ff): the tuner's ff ranges
+        self.ff = None
+        if ff_velocity_gain is not None or ff_acceleration_gain is not None:
+            self.ff = core.ff_rows(
+                m, self.device, True,
+                ff_velocity_gain if ff_velocity_gain is not None else config.get("ff_velocity_gain", 0.0),
+                ff_acceleration_gain if ff_acceleration_gain is not None else config.get("ff_acceleration_gain", 0.0),
+                config.get("ff_max_velocity", 10.0))
 
     def gains(self) -> torch.Tensor:
         return self.K.T.reshape(-1, 4, 6)
@@ -145,6 +154,7 @@ class BatchedLQR:
             return out
         rep = lambda t: None if t is None else t.repeat_interleave(k, dim=-1).contiguous()  # noqa: E731
         out.K, out.mass, out.hover, out.status = rep(self.K), rep(self.mass), rep(self.hover), rep(self.status)
+        out.ff = rep(self.ff)
         out.num_problems = self.num_problems * k
         out.per_episode = True
         return out

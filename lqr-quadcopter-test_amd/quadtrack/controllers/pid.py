@@ -15,7 +15,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .. import _abi
+from .. import _abi, core
 from .base import BaseController
 from .riccati_lqr import _OneEpisodeKernel, _ensure_array, _obs15, _validate_observation, ctrl_params
 
@@ -105,7 +105,7 @@ class BatchedPID:
     k_structured = True
 
     def __init__(self, config: dict | None = None, device=None, *, kp_pos=None, ki_pos=None, kd_pos=None,
-                 mass=None):
+                 mass=None, ff_velocity_gain=None, ff_acceleration_gain=None):
         config = dict(config or {})
         self.config = config
         self.device = _abi.require_gpu(device)
@@ -113,8 +113,9 @@ class BatchedPID:
         base_mass = float(config.get("mass", 1.0))
         if isinstance(mass, torch.Tensor):
             mass = mass.detach().to("cpu", F64).numpy()
-        given = {k: v for k, v in (("kp_pos", kp_pos), ("ki_pos", ki_pos), ("kd_pos", kd_pos), ("mass", mass))
-                 if v is not None}
+        given = {k: v for k, v in (("kp_pos", kp_pos), ("ki_pos", ki_pos), ("kd_pos", kd_pos), ("mass", mass),
+                                   ("ff_velocity_gain", ff_velocity_gain),
+                                   ("ff_acceleration_gain", ff_acceleration_gain)) if v is not None}
         lens = {len(v) for v in given.values()}
         if len(lens) > 1:
             raise ValueError(f"per-episode arrays disagree on the episode count: {sorted(lens)}")
@@ -135,6 +136,14 @@ class BatchedPID:
         self.hover_thrust = base_mass * self.gravity
         self.ctrl = _pid_ctrl(config, self.hover_thrust)
         self.status = torch.zeros(m, dtype=torch.int8, device=self.device)
+        # per-episode feed-forward gains (qt_batch.ff): the tuner's ff ranges
+        self.ff = None
+        if ff_velocity_gain is not None or ff_acceleration_gain is not None:
+            self.ff = core.ff_rows(
+                m, self.device, True,
+                ff_velocity_gain if ff_velocity_gain is not None else config.get("ff_velocity_gain", 0.0),
+                ff_acceleration_gain if ff_acceleration_gain is not None else config.get("ff_acceleration_gain", 0.0),
+                config.get("ff_max_velocity", 10.0))
 
     def gains(self) -> torch.Tensor:
         """[m, 3, 3]: rows kp, ki, kd."""
@@ -148,6 +157,7 @@ class BatchedPID:
             return out
         rep = lambda t: None if t is None else t.repeat_interleave(k, dim=-1).contiguous()  # noqa: E731
         out.K, out.mass, out.hover, out.status = rep(self.K), rep(self.mass), rep(self.hover), rep(self.status)
+        out.ff = rep(self.ff)
         out.num_problems = self.num_problems * k
         out.per_episode = True
         return out

@@ -424,7 +424,7 @@ class BatchedRiccatiLQR:
     kind = "riccati_lqr"
 
     def __init__(self, config: dict | None = None, device=None, *, q_pos=None, q_vel=None, r_controls=None,
-                 q_int=None, mass=None, Q=None, R=None):
+                 q_int=None, mass=None, Q=None, R=None, ff_velocity_gain=None, ff_acceleration_gain=None):
         config = dict(config or {})
         self.config = config
         self.device = _abi.require_gpu(device)
@@ -437,8 +437,9 @@ class BatchedRiccatiLQR:
         base_mass = float(config.get("mass", 1.0))
         if isinstance(mass, torch.Tensor):
             mass = mass.detach().to("cpu", torch.float64).numpy()
-        per = [a is not None for a in (q_pos, q_vel, r_controls, q_int, mass, Q, R)]
-        lens = [len(a) for a in (q_pos, q_vel, r_controls, q_int, mass, Q, R) if a is not None]
+        per_arrays = (q_pos, q_vel, r_controls, q_int, mass, Q, R, ff_velocity_gain, ff_acceleration_gain)
+        per = [a is not None for a in per_arrays]
+        lens = [len(a) for a in per_arrays if a is not None]
         if lens and len(set(lens)) != 1:
             raise ValueError(f"per-episode arrays disagree on the episode count: {lens}")
         m = lens[0] if lens else 1
@@ -500,6 +501,19 @@ class BatchedRiccatiLQR:
                                 config.get("ff_velocity_gain", [0.0, 0.0, 0.0]),
                                 config.get("ff_acceleration_gain", [0.0, 0.0, 0.0]),
                                 config.get("ff_max_velocity", 10.0), config.get("ff_max_acceleration", 5.0))
+        # Per-episode feed-forward (qt_batch.ff): per-candidate gains (the tuner's
+        # ff ranges, controllers/tuning.py:689-735), and the heuristic fallback of a
+        # failed DARE, which runs without feed-forward (riccati_lqr.py:764-776).
+        ff_on = bool(config.get("feedforward_enabled", False)) or ff_velocity_gain is not None or \
+            ff_acceleration_gain is not None
+        self.ff = None
+        if ff_on and (ff_velocity_gain is not None or ff_acceleration_gain is not None or bool(bad.any())):
+            self.ff = core.ff_rows(
+                m, dev, True,
+                ff_velocity_gain if ff_velocity_gain is not None else config.get("ff_velocity_gain", [0.0] * 3),
+                ff_acceleration_gain if ff_acceleration_gain is not None else
+                config.get("ff_acceleration_gain", [0.0] * 3),
+                config.get("ff_max_velocity", 10.0), off=bad.cpu().numpy())
         self.integral_state: torch.Tensor | None = None
 
     @property
@@ -525,6 +539,7 @@ class BatchedRiccatiLQR:
         rep = lambda t: None if t is None else t.repeat_interleave(k, dim=-1).contiguous()  # noqa: E731
         out.K, out.P = rep(self.K), rep(self.P)
         out.status, out.iters, out.mass, out.hover = rep(self.status), rep(self.iters), rep(self.mass), rep(self.hover)
+        out.ff = rep(self.ff)
         out.num_problems = self.num_problems * k
         out.per_episode = True
         out.integral_state = None
@@ -545,5 +560,5 @@ class BatchedRiccatiLQR:
                        t.get("acceleration", torch.zeros_like(t["position"]))], dim=1).T.contiguous()
         if self.integral_state is None or self.integral_state.shape[1] != n:
             self.reset(n)
-        act, _ = core.compute_action(self.ctrl, self.K, self.k_cols, o, self.integral_state, self.hover)
+        act, _ = core.compute_action(self.ctrl, self.K, self.k_cols, o, self.integral_state, self.hover, ff=self.ff)
         return act.T.contiguous()

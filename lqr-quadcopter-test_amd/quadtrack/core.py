@@ -42,6 +42,7 @@ class EpisodeBatch:
     k_structured: bool = False                # every off-axis K entry is exactly zero
     k_no_yaw: bool = False                    # the yaw-rate row of K is exactly zero
     groups: tuple | None = None               # (seg_motion, seg_end): `order` groups slots by motion
+    ff: torch.Tensor | None = None            # [7, n] per-episode feed-forward (qt_batch.ff, ff_rows)
 
     def c_batch(self, with_k=True) -> Batch:
         b = Batch()
@@ -56,6 +57,7 @@ class EpisodeBatch:
         b.k_structured = int(self.k_structured)
         b.k_no_yaw = int(self.k_no_yaw)
         b.order = ptr(self.order)
+        b.ff = ptr(self.ff)
         return b
 
     def select(self, idx: torch.Tensor) -> "EpisodeBatch":
@@ -67,7 +69,7 @@ class EpisodeBatch:
         return EpisodeBatch(n=idx.numel(), device=self.device, pattern=col(self.pattern), offset=col(self.offset), K=K,
                             k_cols=self.k_cols, motion=col(self.motion), plant_mass=col(self.plant_mass),
                             hover=col(self.hover), k_structured=self.k_structured,
-                            k_no_yaw=self.k_no_yaw)
+                            k_no_yaw=self.k_no_yaw, ff=col(self.ff))
 
 
 @dataclass
@@ -92,6 +94,31 @@ class RolloutState:
 
 
 INTEG_ROWS = 4
+FF_ROWS = 7
+
+
+def ff_rows(m: int, device, enabled=True, velocity_gain=0.0, acceleration_gain=0.0, max_velocity=10.0,
+            off=None) -> torch.Tensor:
+    """Per-episode feed-forward parameters (qt_batch.ff, [7, m]): velocity gain
+    xyz, acceleration gain xyz, target-velocity clamp.  velocity_gain /
+    acceleration_gain: scalar, [3] or [m, 3]; enabled: bool or [m]; off: [m]
+    bool (or None) of episodes that run without feed-forward — gains 0 and no
+    clamp, the identity (the heuristic fallback of a failed DARE,
+    riccati_lqr.py:764-776)."""
+    vg = np.broadcast_to(np.asarray(velocity_gain, float).reshape(-1, 3) if np.ndim(velocity_gain) else
+                         np.full(3, float(velocity_gain)), (m, 3))
+    ag = np.broadcast_to(np.asarray(acceleration_gain, float).reshape(-1, 3) if np.ndim(acceleration_gain) else
+                         np.full(3, float(acceleration_gain)), (m, 3))
+    rows = np.empty((FF_ROWS, m))
+    rows[0:3] = vg.T
+    rows[3:6] = ag.T
+    rows[6] = np.broadcast_to(np.asarray(max_velocity, float), (m,))
+    dis = ~np.broadcast_to(np.asarray(enabled, bool), (m,))
+    if off is not None:
+        dis = dis | np.asarray(off, bool).reshape(m)
+    rows[:, dis] = 0.0
+    rows[6, dis] = np.inf
+    return torch.as_tensor(rows, dtype=F64, device=device).contiguous()
 
 
 def gain_rows(k_cols: int) -> int:
@@ -140,6 +167,7 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
     n = batch.n
     _check_cols("pattern", batch.pattern, 4, n)
     _check_cols("offset", batch.offset, 3, n)
+    _check_cols("ff", batch.ff, FF_ROWS, n)
     if batch.k_cols not in (3, 6, 9):
         raise ValueError("k_cols must be 3 (PID), 6 (LQR) or 9 (LQI)")
     rows = gain_rows(batch.k_cols)
@@ -162,9 +190,17 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
         _check_cols("target", st.target, 9, n)
         if st.t.numel() != n:
             raise ValueError("t must have n entries")
-    for t in (batch.pattern, batch.offset, batch.K):
-        if t.device != batch.device or t.dtype != F64:
+    for t in (batch.pattern, batch.offset, batch.K, batch.plant_mass, batch.hover, batch.ff):
+        if t is not None and (t.device != batch.device or t.dtype != F64):
             raise ValueError("batch tensors must be float64 on the batch device")
+    # the kernels read these through raw pointers: dtypes are part of the ABI
+    if batch.motion is not None and (batch.motion.dtype != torch.int8 or batch.motion.device != batch.device):
+        raise ValueError("motion must be an int8 tensor on the batch device")
+    if batch.order is not None:
+        if batch.order.dtype != torch.int32 or batch.order.device != batch.device:
+            raise ValueError("order must be an int32 tensor on the batch device")
+        if torch.unique(batch.order).numel() != n:
+            raise ValueError("order must be a permutation of the episodes")
 
 
 def seed_draws(seeds: torch.Tensor, motion: torch.Tensor | None, motion_default: int):
@@ -332,7 +368,8 @@ def env_step(env: EnvParams, batch: EpisodeBatch, action: torch.Tensor, st: Roll
 
 
 def compute_action(ctrl: CtrlParams, K: torch.Tensor, k_cols: int, obs: torch.Tensor, integ: torch.Tensor,
-                   hover: torch.Tensor | None = None, diag: torch.Tensor | None = None):
+                   hover: torch.Tensor | None = None, diag: torch.Tensor | None = None,
+                   ff: torch.Tensor | None = None):
     """obs [15, n] -> (action [4, n], saturated [n] bool); integ [3, n] updated in place (LQI);
     diag [16, n] (optional) receives the control components.  PID (k_cols 3): obs [16, n] with the
     observation time in row 15, integ [4, n] (integral error, last time), diag [18, n]."""
@@ -351,6 +388,9 @@ def compute_action(ctrl: CtrlParams, K: torch.Tensor, k_cols: int, obs: torch.Te
     b.k_cols = k_cols
     b.k_per_episode = int(K.shape[1] != 1)
     b.hover_thrust = ptr(hover)
+    if ff is not None:
+        _check_cols("ff", ff, FF_ROWS, n)
+    b.ff = ptr(ff)
     act = torch.empty(4, n, dtype=F64, device=dev)
     sat = torch.empty(n, dtype=torch.int8, device=dev)
     with torch.cuda.device(dev):

@@ -248,7 +248,8 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
     b = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pat, dev), offset=core.to_device(off, dev),
                           K=controller.K, k_cols=controller.k_cols, motion=mo, plant_mass=pm, hover=controller.hover,
                           order=od, k_structured=controller.k_structured,
-                          k_no_yaw=core.gains_no_yaw(controller.K, controller.k_cols), groups=groups)
+                          k_no_yaw=core.gains_no_yaw(controller.K, controller.k_cols), groups=groups,
+                          ff=getattr(controller, "ff", None))
     return b
 
 

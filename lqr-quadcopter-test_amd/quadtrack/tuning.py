@@ -18,9 +18,14 @@ fixed order, one `uniform(lo, hi)` per component) and its grid order
 feedback (CMA-ES), result files and resume are the tuner's control plane and
 stay out of scope.
 
-Supported controller_type: "riccati_lqr".  Feed-forward gain ranges need
-per-episode feed-forward gains, which the rollout kernel takes per batch, so
-they raise NotImplementedError.
+Supported controller_type: "riccati_lqr" (per-candidate q_pos / q_vel /
+r_controls / q_int -> one DARE each), "pid" (kp_pos / ki_pos / kd_pos, the
+PIDController of controllers/__init__.py:116-396) and "lqr" (q_pos / q_vel /
+r_thrust / r_rate -> the heuristic gains of LQRController, 522-574), each with
+per-candidate feed-forward gain ranges (qt_batch.ff).  As in the reference,
+a candidate's controller is built from the candidate's keys alone (plus
+`base_controller_config`); keys the controller type does not read are
+ignored, as the reference's controllers ignore them.
 """
 
 from __future__ import annotations
@@ -32,6 +37,8 @@ from itertools import product
 import numpy as np
 import torch
 
+from .controllers.lqr import BatchedLQR
+from .controllers.pid import BatchedPID
 from .controllers.riccati_lqr import BatchedRiccatiLQR
 from .env.config import EnvConfig
 from .rollout import run_closed_loop
@@ -104,12 +111,19 @@ class GainSearchSpace:
 
 
 def default_search_space(controller_type: str = "riccati_lqr") -> GainSearchSpace:
-    """The Riccati-LQR ranges of scripts/controller_autotune.py:375-383 (config 4)."""
-    if controller_type != "riccati_lqr":
-        raise NotImplementedError(f"batched tuning supports riccati_lqr, not {controller_type!r}")
-    return GainSearchSpace(q_pos_range=([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0]),
-                           q_vel_range=([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0]),
-                           r_controls_range=([0.5] * 4, [2.0] * 4))
+    """The default ranges of scripts/controller_autotune.py:360-385 (`get_default_search_space`):
+    PID kp / kd, heuristic-LQR q_pos / q_vel, Riccati-LQR q_pos / q_vel / r_controls (config 4)."""
+    if controller_type == "pid":
+        return GainSearchSpace(kp_pos_range=([0.005, 0.005, 2.0], [0.05, 0.05, 6.0]),
+                               kd_pos_range=([0.02, 0.02, 1.0], [0.15, 0.15, 3.0]))
+    if controller_type == "lqr":
+        return GainSearchSpace(q_pos_range=([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0]),
+                               q_vel_range=([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0]))
+    if controller_type == "riccati_lqr":
+        return GainSearchSpace(q_pos_range=([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0]),
+                               q_vel_range=([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0]),
+                               r_controls_range=([0.5] * 4, [2.0] * 4))
+    return GainSearchSpace()
 
 
 @dataclass
@@ -234,8 +248,6 @@ class BatchedTuner:
     values `_evaluate_config` returns for each (tuning.py:846-928)."""
 
     def __init__(self, config: TuningConfig, device=None, base_controller_config: dict | None = None):
-        if config.controller_type != "riccati_lqr":
-            raise NotImplementedError(f"batched tuning supports riccati_lqr, not {config.controller_type!r}")
         config.search_space.validate()
         self.config = config
         self.device = device
@@ -267,28 +279,55 @@ class BatchedTuner:
         return SuccessCriteria(min_on_target_ratio=0.8, min_episode_duration=self.config.episode_length,
                                target_radius=self.config.target_radius)
 
-    def controller(self, configs: list[dict]) -> BatchedRiccatiLQR:
-        """One batched DARE over the candidates (one problem per candidate)."""
+    # per-candidate keys each controller type reads (its constructor's per-episode arrays)
+    _PER_CANDIDATE = {
+        "riccati_lqr": ("q_pos", "q_vel", "r_controls", "q_int"),
+        "pid": ("kp_pos", "ki_pos", "kd_pos"),
+        "lqr": ("q_pos", "q_vel", "r_thrust", "r_rate"),
+    }
+    _FF_KEYS = ("ff_velocity_gain", "ff_acceleration_gain")
+
+    def controller(self, configs: list[dict]):
+        """One batched controller over the candidates, one gain set (one DARE
+        for riccati_lqr) per candidate (tuning.py:832-844)."""
+        kind = self.config.controller_type
         keys = set().union(*[c.keys() for c in configs]) if configs else set()
-        unsupported = keys & {"ff_velocity_gain", "ff_acceleration_gain", "kp_pos", "ki_pos", "kd_pos",
-                              "r_thrust", "r_rate"}
-        if unsupported:
-            raise NotImplementedError(f"per-candidate {sorted(unsupported)} are not batched")
-        lqi = {bool(c.get("use_lqi", False)) for c in configs}
-        if len(lqi) > 1:
-            raise ValueError("candidates mix LQR and LQI")
         shared = dict(self.base)
-        shared["use_lqi"] = lqi.pop() if lqi else False
+        if kind == "riccati_lqr":
+            lqi = {bool(c.get("use_lqi", False)) for c in configs}
+            if len(lqi) > 1:
+                raise ValueError("candidates mix LQR and LQI")
+            shared["use_lqi"] = lqi.pop() if lqi else False
+        if any(c.get("feedforward_enabled") for c in configs):
+            shared["feedforward_enabled"] = True
 
-        def col(key, default):
-            d = np.asarray(shared.get(key, default), float)
-            return np.stack([np.asarray(c.get(key, d), float) for c in configs])
+        defaults = {"q_pos": [1e-4, 1e-4, 16.0], "q_vel": [0.0036, 0.0036, 4.0], "r_controls": [1.0] * 4,
+                    "q_int": [0.0, 0.0, 0.0], "r_thrust": 1.0, "r_rate": 1.0,
+                    "ff_velocity_gain": [0.0, 0.0, 0.0], "ff_acceleration_gain": [0.0, 0.0, 0.0]}
 
-        kw = dict(q_pos=col("q_pos", [1e-4, 1e-4, 16.0]), q_vel=col("q_vel", [0.0036, 0.0036, 4.0]),
-                  r_controls=col("r_controls", [1.0] * 4))
-        if shared["use_lqi"]:
-            kw["q_int"] = col("q_int", [0.0, 0.0, 0.0])
-        return BatchedRiccatiLQR(shared, device=self.device, **kw)
+        def col(key):
+            if kind == "pid" and key in ("kp_pos", "ki_pos", "kd_pos"):
+                from .controllers.pid import _DEFAULT_KD, _DEFAULT_KI, _DEFAULT_KP
+                d = {"kp_pos": _DEFAULT_KP, "ki_pos": _DEFAULT_KI, "kd_pos": _DEFAULT_KD}[key]
+                alt = key[:2]
+                base = shared.get(key, shared.get(alt, d))
+            else:
+                base = shared.get(key, defaults[key])
+
+            def vec(v):
+                v = np.asarray(v, float)
+                return np.full(3, float(v)) if v.ndim == 0 and key not in ("r_thrust", "r_rate") else v
+            return np.stack([vec(c.get(key, base)) for c in configs])
+
+        kw = {k: col(k) for k in self._PER_CANDIDATE[kind] if k in keys}
+        if kind == "riccati_lqr" and shared["use_lqi"]:
+            kw["q_int"] = col("q_int")
+        if keys & set(self._FF_KEYS):
+            kw.update({k: col(k) for k in self._FF_KEYS})
+        if not kw:  # nothing per candidate: one shared gain set repeated (still one row per candidate)
+            kw = {"mass": np.full(len(configs), float(shared.get("mass", 1.0)))}
+        cls = {"riccati_lqr": BatchedRiccatiLQR, "pid": BatchedPID, "lqr": BatchedLQR}[kind]
+        return cls(shared, device=self.device, **kw)
 
     def evaluate_configs(self, configs: list[dict], chunk: int | None = None):
         """Scores and metrics of every candidate (tuning.py:846-928)."""

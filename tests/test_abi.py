@@ -45,7 +45,7 @@ int main(void) {
   F(qt_env_params, integrator) F(qt_env_params, motion) F(qt_env_params, speed) F(qt_env_params, center)
   F(qt_env_params, min_episode_duration) F(qt_ctrl_params, use_lqi) F(qt_ctrl_params, integral_limit)
   F(qt_ctrl_params, ff_max_acceleration) F(qt_criteria, overshoot_window) F(qt_batch, K) F(qt_batch, k_cols)
-  F(qt_batch, order) F(qt_state, target)
+  F(qt_batch, order) F(qt_batch, ff) F(qt_state, target)
   printf("QT_ACC_ROWS %d\nQT_MET_ROWS %d\n", QT_ACC_ROWS, QT_MET_ROWS);
   return 0;
 }

@@ -79,8 +79,38 @@ def test_search_space_validation():
         tuning.GainSearchSpace(r_controls_range=([1, 1, 1], [2, 2, 2])).validate()
     with pytest.raises(ValueError):
         tuning.TuningConfig(strategy="annealing")
-    with pytest.raises(NotImplementedError):
-        tuning.BatchedTuner(tuning.TuningConfig(controller_type="pid"))
+    with pytest.raises(ValueError, match="Invalid controller_type"):
+        tuning.TuningConfig(controller_type="deep")
+
+
+def test_default_search_spaces_match_autotune_script():
+    """scripts/controller_autotune.py:360-385 (get_default_search_space)."""
+    pid = tuning.default_search_space("pid")
+    assert pid.kp_pos_range == ([0.005, 0.005, 2.0], [0.05, 0.05, 6.0])
+    assert pid.kd_pos_range == ([0.02, 0.02, 1.0], [0.15, 0.15, 3.0])
+    assert pid.get_active_parameters() == ["kp_pos", "kd_pos"]
+    lqr = tuning.default_search_space("lqr")
+    assert lqr.get_active_parameters() == ["q_pos", "q_vel"]
+    ric = tuning.default_search_space("riccati_lqr")
+    assert ric.get_active_parameters() == ["q_pos", "q_vel", "r_controls"]
+    assert tuning.default_search_space("deep").get_active_parameters() == []
+
+
+def test_ff_rows_layout():
+    """qt_batch.ff rows: velocity gain xyz, acceleration gain xyz, velocity
+    clamp; an episode without feed-forward has gains 0 and clamp +inf."""
+    import numpy as np
+    import torch
+
+    from quadtrack import core
+
+    rows = core.ff_rows(3, torch.device("cpu"), True, [0.1, 0.2, 0.3], 0.5, 7.0, off=[False, True, False])
+    r = rows.numpy()
+    assert r.shape == (7, 3)
+    assert r[:, 0].tolist() == [0.1, 0.2, 0.3, 0.5, 0.5, 0.5, 7.0]
+    assert r[:6, 1].tolist() == [0.0] * 6 and np.isinf(r[6, 1])
+    per = core.ff_rows(2, torch.device("cpu"), [True, False], np.array([[1, 2, 3], [4, 5, 6]], float))
+    assert per.numpy()[:3, 0].tolist() == [1, 2, 3] and per.numpy()[:3, 1].tolist() == [0, 0, 0]
 
 
 def test_shard_bounds_partition():
