@@ -42,14 +42,14 @@ FLOPS_PER_ENV_STEP = 429
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, spec (half the FP32 vector 157.3 TF/s)
 HBM_PEAK_GBS = 8000.0
 # the dominant kernel of the bench workload: yaw-at-rest fast flavour, linear target, 6-column structured K
-KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true>"
+KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--episodes", type=int, default=65536, help="episodes per GPU")
     ap.add_argument("--motion", default="linear")
     ap.add_argument("--cpu-sample", type=int, default=65536, help="episodes in the CPU baseline sample (rank 0, N=1)")

@@ -9,7 +9,7 @@ mkdir -p $O
 for step in ${STEPS:-tests bench clock sweep}; do
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; } ;;
-    bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err ;;
+    bench) timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err ;;
     clock) timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 > $O/clock_linear_lqr.json 2> $O/clock.err
            timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 --motion sinusoidal --ctl lqi > $O/clock_sin_lqi.json 2>> $O/clock.err ;;
     sweep) timeout -k 10 300 python scripts/perf_sweep.py --n 65536 --motions ${MOTIONS:-linear,sinusoidal,circular,figure8,stationary,mixed} \

@@ -7,7 +7,7 @@ TAG=${TAG:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 BENCH="bench.py --steps ${PSTEPS:-5} --warmup ${PWARM:-1} --no-cpu-baseline"
-TRACE_BENCH="bench.py --steps ${TSTEPS:-40} --warmup ${TWARM:-10} --no-cpu-baseline"
+TRACE_BENCH="bench.py --steps ${TSTEPS:-200} --warmup ${TWARM:-20} --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $TRACE_BENCH > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 1; }
 # EXTRA_PMC: further passes, separated by ';' (counters within a pass by spaces)
 IFS=';' read -ra EXTRA <<< "${EXTRA_PMC:-}"
