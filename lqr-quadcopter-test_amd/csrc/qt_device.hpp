@@ -323,7 +323,8 @@ __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 // YAW0 (the yaw-at-rest flavour, which is also rate-bounded: rate_bounded_ok)
 // has |delta| <= kRateAngle and takes the shorter rate_sincos.
 template <bool SMALL = false, bool YAW0 = false>
-__device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t) {
+__device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t,
+                                           const RateCoef& rk = RateCoef{}) {
   constexpr int NA = YAW0 ? 2 : 3;
   const double dm = SMALL ? 0.0 : fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
   if (SMALL || dm <= kSmallAngle) {
@@ -331,7 +332,7 @@ __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, co
     for (int i = 0; i < NA; ++i) {
       double sd, cd;
       if (YAW0)
-        rate_sincos(delta[i], &sd, &cd);
+        rate_sincos(delta[i], &sd, &cd, rk);
       else
         small_sincos(delta[i], &sd, &cd);
       t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
@@ -511,11 +512,12 @@ inline LaunchConst make_launch_const(const qt_env_params& e) {
 // carried values are rotated by the exact difference of the rounded angles
 // with rate_sincos (angle addition): they follow sin / cos of the angles the
 // reference evaluates with a drift of a few ulp per step.
-__device__ __forceinline__ void attitude_trig_advance(const double* a_new, double* a_prev, Trig& ta) {
+__device__ __forceinline__ void attitude_trig_advance(const double* a_new, double* a_prev, Trig& ta,
+                                                      const RateCoef& rk = RateCoef{}) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     double sd, cd;
-    rate_sincos(a_new[i] - a_prev[i], &sd, &cd);
+    rate_sincos(a_new[i] - a_prev[i], &sd, &cd, rk);
     const double s0 = ta.s[i], c0 = ta.c[i];
     ta.s[i] = fma(s0, cd, c0 * sd);
     ta.c[i] = fma(c0, cd, -(s0 * sd));
@@ -526,16 +528,16 @@ __device__ __forceinline__ void attitude_trig_advance(const double* a_new, doubl
 // One yaw-at-rest RK4 step in closed form (RateLin, VelLin); x[8], x[11] untouched.
 // ta: sin / cos of roll and pitch at the step start (carried by the caller).
 __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L, const Plant& pl, const Trig& ta,
-                                               double* x, const double* u) {
+                                               double* x, const double* u, const RateCoef& rk = RateCoef{}) {
   const double w0 = x[9], w1 = x[10];
   Trig t[4];
   t[0] = ta;
   const double d2[3] = {R.h2 * w0, R.h2 * w1, 0.0};
   const double d3[3] = {fma(R.d3y, w0, R.d3u * u[1]), fma(R.d3y, w1, R.d3u * u[2]), 0.0};
   const double d4[3] = {fma(R.d4y, w0, R.d4u * u[1]), fma(R.d4y, w1, R.d4u * u[2]), 0.0};
-  trig_shift<true, true>(x + 6, t[0], d2, t[1]);
-  trig_shift<true, true>(x + 6, t[0], d3, t[2]);
-  trig_shift<true, true>(x + 6, t[0], d4, t[3]);
+  trig_shift<true, true>(x + 6, t[0], d2, t[1], rk);
+  trig_shift<true, true>(x + 6, t[0], d3, t[2], rk);
+  trig_shift<true, true>(x + 6, t[0], d4, t[3], rk);
   // thrust direction R3 at each stage (derivatives<true>): (sin th cos phi, -sin phi, cos th cos phi)
   double sv[3] = {0.0, 0.0, 0.0}, sp[3] = {0.0, 0.0, 0.0};
 #pragma unroll

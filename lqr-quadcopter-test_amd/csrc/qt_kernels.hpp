@@ -481,7 +481,9 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   while (a.term == QT_TERM_RUNNING && s < nsteps) {
     const int s0 = s;
     int rem = nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0;  // steps left in this run (z stays < 1 off phase)
+    RateCoef rk;
     do {
+      rk.pin();
       const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_advance)
       // ---- compute_action on the current observation (riccati_lqr.py:779-967)
       double u[4];
@@ -509,7 +511,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       }
       // ---- env.step (quadcopter_env.py:152-232): the command is finite and
       // inside the env clamps, so parsing is the identity
-      integrate_yaw0(k.rl, lin, pl, ta, x, u);
+      integrate_yaw0(k.rl, lin, pl, ta, x, u, rk);
       const double t0 = t;
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
@@ -529,7 +531,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       const bool vbad = !(x[3] * x[3] + x[4] * x[4] + x[5] * x[5] < vm2);
       if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
       double ap[2] = {a0[0], a0[1]};
-      attitude_trig_advance(x + 6, ap, ta);
+      attitude_trig_advance(x + 6, ap, ta, rk);
       const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
       const bool tl = t >= e.max_episode_time;
       --rem;

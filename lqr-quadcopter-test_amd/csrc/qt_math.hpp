@@ -117,14 +117,27 @@ QT_HD void sincos_tilt(double a, double* s, double* c) {
 // d^6, truncation below 8e-20 (sin) and 2.2e-17 (cos, the d^8 / 8! term).
 constexpr double kRateAngle = 0.031;
 
-QT_HD void rate_sincos(double d, double* s, double* c) {
+// The two leading coefficients as values: a loop can hold them in vector
+// registers (RateCoef::pin), since an fma takes one scalar-register operand
+// and the next coefficient already is one.
+struct RateCoef {
+  double s7 = -1.9841269841269841e-04;  // -1/7!
+  double c6 = -1.3888888888888889e-03;  // -1/6!
+#if defined(__HIP_DEVICE_COMPILE__)
+  // opaque to the optimiser: kept in VGPRs across a loop instead of being
+  // re-materialised from scalar registers each trip (no instruction emitted)
+  __device__ __forceinline__ void pin() { asm("" : "+v"(s7), "+v"(c6)); }
+#else
+  void pin() {}
+#endif
+};
+
+QT_HD void rate_sincos(double d, double* s, double* c, const RateCoef& k = RateCoef{}) {
   const double z = d * d;
-  double p = -1.9841269841269841e-04;     // -1/7!
-  p = fma(z, p, 8.3333333333333332e-03);  // 1/5!
+  double p = fma(z, k.s7, 8.3333333333333332e-03);  // 1/5!
   p = fma(z, p, -1.6666666666666666e-01);  // -1/3!
   *s = fma(d * z, p, d);
-  double q = -1.3888888888888889e-03;     // -1/6!
-  q = fma(z, q, 4.1666666666666664e-02);  // 1/4!
+  double q = fma(z, k.c6, 4.1666666666666664e-02);  // 1/4!
   q = fma(z, q, -0.5);
   *c = fma(z, q, 1.0);
 }

@@ -1,0 +1,28 @@
+#!/bin/bash
+# rocprofv3 kernel trace + one SQ counter pass for the secondary workloads:
+# config 3 (LQI, sinusoidal), config 5 (1M episodes, grouped motions, one
+# launch), and the batched DARE kernels (scripts/dare_bench.py).  Every step is
+# time-limited; the first failure ends the script.  Outputs under
+# gpurun_out/profw_<tag>/<case>_{trace,sq}/.
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r02}
+OUT=gpurun_out/profw_$TAG
+mkdir -p $OUT
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU"
+run_case() {  # name, then the python arguments
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${name}_trace -o run -- python3 "$@" \
+    > $OUT/${name}_trace.log 2>&1 || { echo "$name trace failed"; tail -20 $OUT/${name}_trace.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/${name}_sq -o run -- python3 "$@" \
+    > $OUT/${name}_sq.log 2>&1 || { echo "$name sq failed"; tail -20 $OUT/${name}_sq.log; exit 1; }
+  echo "$name done"
+}
+for c in ${CASES:-cfg3 cfg5 dare}; do
+  case $c in
+    cfg3) run_case cfg3 scripts/run_workload.py --config 3 --repeat 10 ;;
+    cfg5) run_case cfg5 scripts/run_workload.py --config 5 --repeat 5 ;;
+    dare) run_case dare scripts/dare_bench.py --reps 5 ;;
+  esac
+done
