@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 3
+#define QT_ABI_VERSION 4
 
 /* error codes */
 #define QT_OK 0
@@ -180,6 +180,20 @@ typedef struct qt_state {
 
 /* ABI version of the loaded library. */
 int qt_abi_version(void);
+
+/* Page-locked host memory mapped into the devices' address space (zero copy):
+   *host and *dev address the same zeroed bytes.  The batch-1 drop-in objects
+   (QuadcopterEnv, the one-episode controllers) keep their per-episode arrays
+   here and pass *dev pointers to the entry points below, so a reference-style
+   step is one launch and one qt_stream_sync with no copies.  Kernel writes are
+   visible to the host after qt_stream_sync.  Not a replacement of any
+   reference interface: the reference's env and controller hold numpy arrays
+   (quadcopter_env.py:99-109, riccati_lqr.py:779-967). */
+int qt_host_alloc(int64_t bytes, void** host, void** dev);
+int qt_host_free(void* host);
+
+/* hipStreamSynchronize(stream): waits for the stream's launches. */
+int qt_stream_sync(void* stream);
 
 /* QuadcopterEnv.reset(seed) from pre-drawn randoms (quadcopter_env.py:111-150):
    x = [p_target(0) + offset, 0...], t = 0, accumulators cleared, target row

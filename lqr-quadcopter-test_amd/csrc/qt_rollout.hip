@@ -8,6 +8,7 @@
 // instantiated in qt_rollout_fast.hip.
 // Reference functions: src/quadcopter_tracking/... of the reference repo.
 #include "qt_kernels.hpp"
+#include <cstring>
 
 using namespace qtk;
 
@@ -413,6 +414,29 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
 extern "C" {
 
 int qt_abi_version(void) { return QT_ABI_VERSION; }
+
+int qt_host_alloc(int64_t bytes, void** host, void** dev) {
+  if (bytes <= 0 || !host || !dev) return QT_EINVAL;
+  void* h = nullptr;
+  // fine-grained (coherent) and mapped into every device's address space
+  if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+      hipSuccess)
+    return QT_ELAUNCH;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return QT_ELAUNCH;
+  }
+  memset(h, 0, (size_t)bytes);
+  *host = h, *dev = d;
+  return 0;
+}
+
+int qt_host_free(void* host) { return host && hipHostFree(host) == hipSuccess ? 0 : QT_EINVAL; }
+
+int qt_stream_sync(void* stream) {
+  return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? 0 : QT_ELAUNCH;
+}
 
 
 int qt_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, qt_state st, void* stream) {

@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
 LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # enums (include/quadtrack.h)
 MOTIONS = ("stationary", "linear", "circular", "sinusoidal", "figure8")
@@ -79,7 +79,7 @@ class State(C.Structure):
                 ("target", C.c_void_p)]
 
 
-EXPORTS = ("qt_abi_version", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_grouped",
+EXPORTS = ("qt_abi_version", "qt_host_alloc", "qt_host_free", "qt_stream_sync", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_grouped",
            "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary",
            "qt_summary_parts")
@@ -102,6 +102,9 @@ def load():
     L = C.CDLL(LIB_PATH)
     P, vp, i32, i64, dbl = C.POINTER, C.c_void_p, C.c_int32, C.c_int64, C.c_double
     L.qt_abi_version.restype = C.c_int
+    L.qt_host_alloc.argtypes = [i64, P(vp), P(vp)]
+    L.qt_host_free.argtypes = [vp]
+    L.qt_stream_sync.argtypes = [vp]
     L.qt_seed_draws.argtypes = [i64, vp, vp, i32, vp, vp, vp]
     L.qt_reset.argtypes = [P(EnvParams), P(Batch), vp, State, vp]
     L.qt_rollout.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, vp]

@@ -14,6 +14,7 @@
 
 from __future__ import annotations
 
+import ctypes as C
 import logging
 
 import numpy as np
@@ -196,35 +197,42 @@ def _validate_observation(observation: dict) -> None:
 
 
 class _OneEpisodeKernel:
-    """Device buffers for running qt_compute_action on one observation.
-    One upload (obs, plus the integral state when the host owns it) and one
-    download (action | integral | diagnostics | saturation flag) per call.
-    Integral / diagnostics: 3 / 16 values (LQR, LQI), 4 / 18 (PID: integral
-    error + last observation time; p, i, d, ff terms, total correction)."""
+    """qt_compute_action on one observation, its inputs and outputs in mapped
+    page-locked host memory (core.MappedBlock): a call is one launch and one
+    stream sync, no copies; the gains stay in device memory.
+    Output row: action (4) | integral (3 LQR/LQI; 4 PID: integral error + last
+    observation time) | diagnostics (16; 18 PID: p, i, d, ff terms, total
+    correction) | saturation flag."""
 
     def __init__(self, K: np.ndarray, k_cols: int, device):
         self.dev = _abi.require_gpu(device)
         self.k_cols = k_cols
         self.ni, self.nd = (4, 18) if k_cols == 3 else (3, 16)
         self.K = torch.as_tensor(np.ascontiguousarray(K[:, :k_cols].reshape(-1, 1)), dtype=F64, device=self.dev)
-        self.buf = torch.zeros(4 + self.ni + self.nd + 1, dtype=F64, device=self.dev)
+        blk = self._blk = core.MappedBlock(1024)
+        self.buf, buf_d = blk.take(4 + self.ni + self.nd + 1)
+        self.obs, self.obs_d = blk.take(16)
+        self.sat, self.sat_d = blk.take(1, np.int8)
+        self.act_d = buf_d
+        self.integ_d = C.c_void_p(buf_d.value + 4 * 8)
+        self.diag_d = C.c_void_p(buf_d.value + (4 + self.ni) * 8)
+        self.batch = _abi.Batch()
+        self.batch.n, self.batch.K, self.batch.k_cols = 1, _abi.ptr(self.K), k_cols
 
     def zero_integral(self):
-        self.buf[4:7].zero_()
+        self.buf[4:7] = 0.0
 
     def __call__(self, ctrl: CtrlParams, obs: np.ndarray, integ: np.ndarray | None = None):
         no = obs.size
-        host = obs if integ is None else np.concatenate([obs, integ])
-        up = torch.as_tensor(np.ascontiguousarray(host, dtype=np.float64).reshape(-1, 1)).to(self.dev)
-        b = self.buf
-        i0, d0 = 4, 4 + self.ni
+        self.obs[:no] = obs
         if integ is not None:
-            b[i0:d0].copy_(up[no:, 0])
-        act, sat = core.compute_action(ctrl, self.K, self.k_cols, up[:no], b[i0:d0].view(self.ni, 1), None,
-                                       b[d0:d0 + self.nd].view(self.nd, 1))
-        b[0:4].copy_(act.view(4))
-        b[-1] = sat.to(F64)[0]
-        return b.cpu().numpy()
+            self.buf[4:4 + self.ni] = integ
+        s = _abi.stream_of(self.dev)
+        _abi.check(_abi.load().qt_compute_action(C.byref(ctrl), C.byref(self.batch), self.obs_d, self.integ_d,
+                                                 self.act_d, self.sat_d, self.diag_d, s), "qt_compute_action")
+        core.sync(s)
+        self.buf[-1] = float(self.sat[0])
+        return self.buf.copy()
 
 
 def _obs15(observation: dict) -> np.ndarray:

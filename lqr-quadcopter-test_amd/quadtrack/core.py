@@ -151,6 +151,40 @@ def gains_no_yaw(K: torch.Tensor, k_cols: int) -> bool:
     return bool((K[3 * k_cols:4 * k_cols] == 0).all().item())
 
 
+class MappedBlock:
+    """Page-locked host memory mapped into the device address space
+    (qt_host_alloc): numpy views on the host side, device pointers for the
+    kernels, no copies.  `take` carves 64-byte aligned arrays out of it.
+    Used by the batch-1 drop-in objects, whose every call is one launch and
+    one stream sync (QuadcopterEnv, the one-episode controllers)."""
+
+    def __init__(self, nbytes: int):
+        self._lib = _abi.load()
+        host, dev = C.c_void_p(), C.c_void_p()
+        check(self._lib.qt_host_alloc(int(nbytes), C.byref(host), C.byref(dev)), "qt_host_alloc")
+        self.host, self.dev, self.nbytes, self._off = host.value, dev.value, int(nbytes), 0
+        self._raw = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.host))
+
+    def take(self, shape, dtype=np.float64):
+        """A zeroed array of `shape` and its device address."""
+        dt = np.dtype(dtype)
+        size = int(np.prod(shape)) * dt.itemsize
+        off = self._off
+        if off + size > self.nbytes:
+            raise ValueError("MappedBlock exhausted")
+        self._off = (off + size + 63) & ~63
+        return self._raw[off:off + size].view(dt).reshape(shape), C.c_void_p(self.dev + off)
+
+    def __del__(self):
+        if getattr(self, "host", None):
+            self._lib.qt_host_free(C.c_void_p(self.host))
+            self.host = None
+
+
+def sync(stream) -> None:
+    check(_abi.load().qt_stream_sync(stream), "qt_stream_sync")
+
+
 def to_device(a, device, dtype=F64) -> torch.Tensor:
     if isinstance(a, torch.Tensor):
         return a.to(device=device, dtype=dtype).contiguous()

@@ -4,8 +4,10 @@
 Same constructor, reset/step signatures, observation dict (fresh numpy
 copies), info keys, exceptions, history and violation records.  The physics
 (action validation, RK4/Euler, constraints, target, error, termination) runs
-in the HIP step kernel on a one-episode `BatchedQuadcopterEnv`; the host side
-keeps only the reference's bookkeeping (counters, violation strings, history).
+in the HIP reset / step kernels (qt_reset, qt_env_step) on a one-episode
+state kept in mapped page-locked host memory (core.MappedBlock): a step is
+one launch and one stream sync, with no copies; the host side keeps only the
+reference's bookkeeping (counters, violation strings, history).
 Seeding follows the reference exactly: the env and target streams are
 `numpy.random.default_rng` generators re-created on a seeded reset and
 continued on an unseeded one (quadcopter_env.py:108-139).
@@ -13,13 +15,13 @@ continued on an unseeded one (quadcopter_env.py:108-139).
 
 from __future__ import annotations
 
+import ctypes as C
 import logging
 
 import numpy as np
-import torch
 
-from .._abi import ACC_ON_POST, ACC_STEPS, TERM_REASONS
-from .batched import BatchedQuadcopterEnv
+from .. import _abi, core
+from .._abi import ACC_ON_POST, ACC_ROWS, ACC_STEPS, TERM_REASONS, Batch, State
 from .config import EnvConfig, as_env_config
 from .target_motion import TargetMotion
 
@@ -36,8 +38,25 @@ class QuadcopterEnv:
 
     def __init__(self, config: dict | EnvConfig | None = None, device=None):
         self.config = as_env_config(config)
+        self.params = self.config.to_params()
+        self.device = _abi.require_gpu(device)
         self.target = TargetMotion(params=self.config.target, seed=self.config.seed)
-        self._dev = BatchedQuadcopterEnv(1, self.config, device=device)
+        # the one episode's arrays (qt_state / qt_batch with n = 1), mapped for the kernels
+        blk = self._blk = core.MappedBlock(4096)
+        self._x, x_d = blk.take(12)
+        self._integ, integ_d = blk.take(core.INTEG_ROWS)
+        self._t, t_d = blk.take(1)
+        self._acc, acc_d = blk.take(ACC_ROWS)
+        self._tg, tg_d = blk.take(9)
+        self._pat, pat_d = blk.take(4)
+        self._off, self._off_d = blk.take(3)
+        self._act, self._act_d = blk.take(4)
+        self._err, self._err_d = blk.take(1)
+        self._flags, flags_d = blk.take(4, np.int8)  # on_target, done, term, violation
+        self._flag_d = [C.c_void_p(flags_d.value + i) for i in range(4)]
+        self._cstate = State(x_d, integ_d, t_d, acc_d, tg_d)
+        self._cbatch = Batch()
+        self._cbatch.n, self._cbatch.pattern, self._cbatch.k_cols = 1, pat_d, 6
         self._state_vector = np.zeros(self.STATE_DIM)
         self._target_obs = np.zeros(9)
         self._time = 0.0
@@ -49,15 +68,20 @@ class QuadcopterEnv:
         self._total_steps = 0
         self._rng = np.random.default_rng(self.config.seed)
 
+    def _stream(self):
+        return _abi.stream_of(self.device)
+
     # ----------------------------------------------------------------- reset
     def reset(self, seed: int | None = None) -> dict:
         if seed is not None:
             self._rng = np.random.default_rng(seed)
             self.target = TargetMotion(params=self.config.target, seed=seed)
         self.target.reset(seed=seed)
-        offset = self._rng.uniform(-0.5, 0.5, 3)
-        pat = self.target.raw_draws.reshape(4, 1)
-        self._dev.reset_from_draws(pat, offset.reshape(3, 1))
+        self._off[:] = self._rng.uniform(-0.5, 0.5, 3)
+        self._pat[:] = np.asarray(self.target.raw_draws, dtype=np.float64).reshape(4)
+        lib, s = _abi.load(), self._stream()
+        _abi.check(lib.qt_reset(C.byref(self.params), C.byref(self._cbatch), self._off_d, self._cstate, s), "qt_reset")
+        core.sync(s)
         self._pull()
         self._time = 0.0
         self._step_count = 0
@@ -69,10 +93,8 @@ class QuadcopterEnv:
         return self._get_observation()
 
     def _pull(self):
-        st = self._dev.state
-        packed = torch.cat([st.x[:, 0], st.target[:, 0]]).cpu().numpy()
-        self._state_vector = packed[:12].copy()
-        self._target_obs = packed[12:21].copy()
+        self._state_vector = self._x.copy()
+        self._target_obs = self._tg.copy()
 
     # ------------------------------------------------------------------ step
     def _parse_action(self, action) -> tuple[np.ndarray, list[str]]:
@@ -107,16 +129,15 @@ class QuadcopterEnv:
         vec, violations = self._parse_action(action)
         if violations:
             self._action_violations.append({"step": self._step_count, "time": self._time, "violations": violations})
-        _, reward_t, done_t, info_t = self._dev.step(torch.as_tensor(vec.reshape(1, 4)))
-        st = self._dev.state
-        packed = torch.cat([st.x[:, 0], st.target[:, 0], st.t, info_t["tracking_error"],
-                            info_t["termination_code"].to(torch.float64), info_t["violation"].to(torch.float64)]
-                           ).cpu().numpy()
-        self._state_vector = packed[:12].copy()
-        self._target_obs = packed[12:21].copy()
-        self._time = float(packed[21])
-        err = float(packed[22])
-        term = int(packed[23])
+        self._act[:] = vec
+        lib, s, f = _abi.load(), self._stream(), self._flag_d
+        _abi.check(lib.qt_env_step(C.byref(self.params), C.byref(self._cbatch), self._act_d, self._cstate,
+                                   self._err_d, f[0], f[1], f[2], f[3], s), "qt_env_step")
+        core.sync(s)
+        self._pull()
+        self._time = float(self._t[0])
+        err = float(self._err[0])
+        term = int(self._flags[2])
         applied = self._applied_action(vec)
         self._step_count += 1
         self._total_steps += 1
@@ -210,7 +231,7 @@ class QuadcopterEnv:
         if state.shape != (self.STATE_DIM,):
             raise ValueError(f"State must have shape ({self.STATE_DIM},), got {state.shape}")
         self._state_vector = state.copy()
-        self._dev.set_state_vector(state.reshape(1, self.STATE_DIM))
+        self._x[:] = state  # the kernels read the mapped state directly
 
     @staticmethod
     def hover_action(mass: float = 1.0, gravity: float = 9.81) -> dict:

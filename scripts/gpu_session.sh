@@ -20,6 +20,7 @@ for step in ${STEPS:-tests bench clock sweep}; do
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     profile) TAG=${TAG:-run} timeout -k 10 900 scripts/profile_session.sh > $O/profile.log 2>&1 ;;
     profw) TAG=${TAG:-run} timeout -k 10 900 scripts/profile_workloads.sh > $O/profw.log 2>&1 || { tail -20 $O/profw.log; exit 1; } ;;
+    dropin) timeout -k 10 300 python scripts/dropin_loop.py > $O/dropin.jsonl 2> $O/dropin.err ;;
     dare) timeout -k 10 120 python scripts/dare_bench.py > $O/dare.jsonl 2> $O/dare.err ;;
   esac
   echo "$step done"
