@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "../../include/quadtrack.h"
+#include "qt_crtrig.hpp"
 #include "qt_math.hpp"
 
 namespace qt {
@@ -27,7 +28,14 @@ __device__ __forceinline__ double clipd(double v, double lo, double hi) {
   return r > hi ? hi : r;
 }
 
-__device__ __forceinline__ double norm3(double a, double b, double c) { return sqrt(a * a + b * b + c * c); }
+// np.linalg.norm of a 1-D 3-vector: sqrt(v.dot(v)), and the image's OpenBLAS
+// ddot accumulates with FMA, i.e. sqrt(fma(c, c, fma(b, b, a * a))) (the
+// reference's velocity clamp, acceleration clamp, direction normalisation,
+// feed-forward magnitudes and LQI error norm; quadcopter_env.py:443,
+// target_motion.py:47, 321, 403, riccati_lqr.py:839, 858, 873).  Metrics
+// rows (np.linalg.norm(..., axis=1)) are plain sums instead (sq3_ref).
+__device__ __forceinline__ double dot3_blas(double a, double b, double c) { return fma(c, c, fma(b, b, a * a)); }
+__device__ __forceinline__ double norm3(double a, double b, double c) { return sqrt(dot3_blas(a, b, c)); }
 
 // np.sign equality used by the LQI anti-windup (riccati_lqr.py:881-883):
 // sign(NaN) is NaN, which equals nothing.
@@ -185,9 +193,18 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     fast_sincos(pt.o0 * t, &st, &ct);
     figure8_recip(e, pt.o0, st, ct, o);
   } else if (motion == QT_MOTION_FIGURE8) {
+    // With the acceleration wanted (feed-forward) the forward difference
+    // below multiplies the positions' last bit by ~1e12, so they are formed
+    // as numpy forms them: sin / cos correctly rounded (cr_sincos; glibc's,
+    // the reference's, round correctly but for ~0.15% of arguments) and no
+    // FMA contraction (1 + sin^2 contracted is not 1 + fl(sin^2)).
+#pragma clang fp contract(off)
     const double sc = e.amplitude, om = pt.o0;
     double st, ct;
-    fast_sincos(om * t, &st, &ct);
+    if (WANT_ACC)
+      cr_sincos(om * t, &st, &ct);
+    else
+      fast_sincos(om * t, &st, &ct);
     double den = 1.0 + st * st;
     double dcos = -st * om, dsin = ct * om;
     double dden = 2.0 * st * dsin;
@@ -201,7 +218,7 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;
       double stp, ctp;
-      fast_sincos(om * (t + h), &stp, &ctp);
+      cr_sincos(om * (t + h), &stp, &ctp);
       double denp = 1.0 + stp * stp;
       double pp0 = e.center[0] + sc * ctp / denp;
       double pp1 = e.center[1] + sc * stp * ctp / denp;
@@ -655,7 +672,7 @@ __device__ __forceinline__ bool norm_le(double s, double r) {
 // construction (finite reset, finite clipped actions, bounded updates).
 template <bool EXACT_NAN = true>
 __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
-  const double s = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
+  const double s = dot3_blas(x[3], x[4], x[5]);
   if (norm_gt(s, e.max_velocity)) {
     const double vm = sqrt(s);
 #pragma unroll

@@ -419,7 +419,7 @@ __device__ __forceinline__ void rotor_target_rt(const qt_env_params& e, const La
 // constrain_fast_apply (rates stay inside their clamp, angles inside the
 // wrap's range: rate_bounded_ok, trig_of<true>).
 __device__ __forceinline__ void clamp_velocity(const qt_env_params& e, double* x) {
-  const double s = x[3] * x[3] + x[4] * x[4] + x[5] * x[5];
+  const double s = dot3_blas(x[3], x[4], x[5]);
   if (norm_gt(s, e.max_velocity)) {
     const double vm = sqrt(s);
 #pragma unroll
@@ -630,6 +630,9 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     if ((threadIdx.x & 63) == 0 && wave < kStampWaves) {
       g_qt_stamps[wave][0] = t0, g_qt_stamps[wave][1] = t1;
       g_qt_stamps[wave][2] = r0, g_qt_stamps[wave][3] = r1;
+      // where the wave ran: HW_ID (wave, SIMD, CU, SH, SE fields) and the XCD
+      g_qt_stamps[wave][4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      g_qt_stamps[wave][5] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);
     }
 #endif
   } else {

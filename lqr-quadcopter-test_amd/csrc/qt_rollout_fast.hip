@@ -19,7 +19,7 @@
 // its own, which no other code reads; qt_debug_stamps copies it out.  The
 // product build has QT_CLOCK_STAMP == 0 and executes no stamp.
 constexpr int kStampWaves = 1 << 16;
-__device__ unsigned long long g_qt_stamps[kStampWaves][4];
+__device__ unsigned long long g_qt_stamps[kStampWaves][6];  // memtime x2, realtime x2, HW_ID, XCC_ID
 #endif
 
 #include "qt_kernels.hpp"
@@ -69,7 +69,7 @@ extern "C" {
 // {memtime start, end, realtime start, end} to host memory out[waves][4].
 int qt_debug_stamps(unsigned long long* out, int64_t waves) {
   if (!out || waves < 0 || waves > kStampWaves) return QT_EINVAL;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 4 * waves) == hipSuccess
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), sizeof(unsigned long long) * 6 * waves) == hipSuccess
              ? QT_OK
              : QT_ELAUNCH;
 }

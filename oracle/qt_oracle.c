@@ -27,7 +27,13 @@
 #define OQ_TWO_PI 6.283185307179586 /* 2 * np.pi */
 
 static double sq(double v) { return v * v; }
-static double norm3(const double* v) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+/* np.linalg.norm of a 1-D 3-vector is sqrt(x.dot(x)), and this image's
+   OpenBLAS ddot accumulates with FMA: sqrt(fma(z, z, fma(y, y, x * x)))
+   (identical to numpy on 20,000 random vectors; the plain sum differs in
+   ~11%).  norm3_rows: np.linalg.norm(..., axis=1) of the metrics
+   (utils/metrics.py:162), a plain left-to-right sum of squares. */
+static double norm3(const double* v) { return sqrt(fma(v[2], v[2], fma(v[1], v[1], v[0] * v[0]))); }
+static double norm3_rows(const double* v) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 /* np.clip = minimum(maximum(a, lo), hi), NaN-propagating */
 static double clipd(double v, double lo, double hi) {
   double r = v;
@@ -64,8 +70,8 @@ void oq_target_state(const qt_env_params* e, int motion, const double* pat, doub
     p[1] = e->center[1] + e->radius * s;
     v[0] = -e->radius * om * s;
     v[1] = e->radius * om * c;
-    a[0] = -e->radius * (om * om) * c;
-    a[1] = -e->radius * (om * om) * s;
+    a[0] = -e->radius * pow(om, 2.0) * c; /* omega**2: Python's float pow (libm), */
+    a[1] = -e->radius * pow(om, 2.0) * s; /* not always om * om rounded */
   } else if (motion == QT_MOTION_SINUSOIDAL) {
     /* _create_pattern 337-359, SinusoidalMotion 118-150 */
     double amp[3] = {e->amplitude, e->amplitude * 0.5, e->amplitude * 0.25};
@@ -76,26 +82,29 @@ void oq_target_state(const qt_env_params* e, int motion, const double* pat, doub
       double s = sin(th), c = cos(th);
       p[i] = e->center[i] + amp[i] * s;
       v[i] = amp[i] * om * c;
-      a[i] = -amp[i] * (om * om) * s;
+      a[i] = -amp[i] * (om * om) * s; /* omega is an ndarray: omega**2 is np.square */
     }
   } else if (motion == QT_MOTION_FIGURE8) {
     /* Figure8Motion 153-231 (scale = amplitude) */
     double sc = e->amplitude, om = e->speed / sc;
     double th = om * t;
     double ct = cos(th), st = sin(th);
-    double den = 1.0 + st * st;
+    /* sin_t**2, denom**2: numpy float64 scalar power = libm pow, which
+       rounds x^2 differently from x * x in ~0.2% of arguments */
+    double den = 1.0 + pow(st, 2.0);
     p[0] = e->center[0] + sc * ct / den;
     p[1] = e->center[1] + sc * st * ct / den;
     double dcos = -st * om, dsin = ct * om;
     double dden = 2.0 * st * dsin;
-    double dx = (dcos * den - ct * dden) / (den * den);
-    double dy = ((dsin * ct + st * dcos) * den - st * ct * dden) / (den * den);
+    double den2 = pow(den, 2.0);
+    double dx = (dcos * den - ct * dden) / den2;
+    double dy = ((dsin * ct + st * dcos) * den - st * ct * dden) / den2;
     v[0] = sc * dx;
     v[1] = sc * dy;
     double h = 1e-6;
     double thp = om * (t + h);
     double ctp = cos(thp), stp = sin(thp);
-    double denp = 1.0 + stp * stp;
+    double denp = 1.0 + pow(stp, 2.0);
     double pp0 = e->center[0] + sc * ctp / denp;
     double pp1 = e->center[1] + sc * stp * ctp / denp;
     a[0] = ((pp0 - p[0]) / h - v[0]) / h;
@@ -390,7 +399,7 @@ void oq_episode(const qt_env_params* e, const qt_ctrl_params* c, const qt_criter
     }
     /* pre-step record (eval.py:142-159) */
     double d[3] = {tgt[0] - x[0], tgt[1] - x[1], tgt[2] - x[2]};
-    double ep = norm3(d);
+    double ep = norm3_rows(d);
     sum_e += ep;
     sum_e2 += ep * ep;
     if (!(ep <= max_e)) max_e = (isnan(max_e) ? max_e : ep);

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--motion", default="linear")
     ap.add_argument("--ctl", default="lqr")
     ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--dump", default="", help="write the per-wave stamps to this .npz")
     args = ap.parse_args()
     if "QUADTRACK_LIB" not in os.environ:
         os.environ["QUADTRACK_LIB"] = os.path.join(ROOT, "build", "stamp", "libquadtrack.so")
@@ -70,7 +71,7 @@ def main():
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     waves = (n + 63) // 64
-    buf = np.zeros((waves, 4), dtype=np.uint64)
+    buf = np.zeros((waves, 6), dtype=np.uint64)
     _abi.check(lib.qt_debug_stamps(buf.ctypes.data, waves), "qt_debug_stamps")
     dt = (buf[:, 1] - buf[:, 0]).astype(np.float64)
     dr = (buf[:, 3] - buf[:, 2]).astype(np.float64)
@@ -85,6 +86,24 @@ def main():
            "loop_ms_max": round(float(np.max(dr[ok])) / 1e5, 4),
            "kernel_ms_last10_median": round(float(np.median(ms[-10:])), 4),
            "kernel_ms_first": round(float(ms[0]), 4)}
+    # where the slow waves ran: loop time by XCD and by SIMD-occupancy of their CU
+    hw, xcc = buf[:, 4].astype(np.int64), buf[:, 5].astype(np.int64) & 0xF
+    cu_key = (xcc << 16) | (((hw >> 13) & 0x7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
+    simd_key = (cu_key << 2) | ((hw >> 4) & 3)
+    _, simd_inv, simd_cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+    out["waves_per_simd_max"] = int(simd_cnt.max())
+    out["simds_used"] = int(len(simd_cnt))
+    out["loop_ms_by_xcd"] = {int(x): round(float(np.median(dr[xcc == x])) / 1e5, 4) for x in np.unique(xcc)}
+    out["loop_ms_max_by_xcd"] = {int(x): round(float(np.max(dr[xcc == x])) / 1e5, 4) for x in np.unique(xcc)}
+    out["clock_mhz_by_xcd"] = {int(x): round(float(np.median((dt / dr * 100.0)[xcc == x])), 1) for x in np.unique(xcc)}
+    shared = simd_cnt[simd_inv] > 1
+    out["loop_ms_shared_simd_median"] = round(float(np.median(dr[shared])) / 1e5, 4) if shared.any() else None
+    start = (buf[:, 2].astype(np.float64) - buf[:, 2].min()) / 1e5
+    end = (buf[:, 3].astype(np.float64) - buf[:, 2].min()) / 1e5
+    out["start_ms_p50_p99_max"] = [round(float(v), 4) for v in np.percentile(start, [50, 99, 100])]
+    out["end_ms_p50_p99_max"] = [round(float(v), 4) for v in np.percentile(end, [50, 99, 100])]
+    if args.dump:
+        np.savez(args.dump, stamps=buf)
     print(json.dumps(out), flush=True)
 
 

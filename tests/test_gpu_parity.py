@@ -2,10 +2,14 @@
 golden fixtures and the CPU oracle on identical seeded inputs.
 
 Tolerance (north star): 1e-5 absolute on states and per-episode metrics in
-FP64.  Exceptions, both inherited from the reference's own numerics:
-figure-8 feed-forward runs (1e-6 finite-difference acceleration, ~1e-4
-noise) and the sub-ulp DARE differences between scipy's QZ solver and the
-doubling algorithm (gains compared at rtol 1e-8).
+FP64.  Exceptions, both inherited from the reference's own numerics: the
+figure-8 feed-forward run, whose 1e-6 nested forward-difference acceleration
+(target_motion.py:215-229) multiplies the last bit of sin / cos / x**2 by
+~1e12 — the device evaluates them correctly rounded (cr_sincos) where glibc
+misrounds ~0.15% of arguments; measured (scripts/ff_fig8_deviation.py):
+final states 2.7e-5, metrics 1.3e-8 relative — and the sub-ulp DARE
+differences between scipy's QZ solver and the doubling algorithm (gains
+compared at rtol 1e-8).
 """
 
 import json
@@ -25,7 +29,7 @@ SCEN = json.load(open(os.path.join(GOLDEN, "scenarios.json")))
 CL = np.load(os.path.join(GOLDEN, "closed_loop.npz"))
 FIELDS = SCEN["metric_fields"]
 TOL = 1e-5
-FF_FIG8_TOL = 2e-3
+FF_FIG8_TOL = 1e-4
 
 
 @pytest.fixture(scope="module")
@@ -55,7 +59,7 @@ def test_fused_rollout_matches_reference(qt, s):
     n = len(s["seeds"])
     envs, ctls = _cfg_list(s, "env", n), _cfg_list(s, "ctl", n)
     tol = FF_FIG8_TOL if s["name"] == "ff_figure8" else TOL
-    rtol = 1e-5 if s["name"] == "ff_figure8" else 1e-8
+    rtol = 1e-7 if s["name"] == "ff_figure8" else 1e-8
     # one batch per distinct env config (config 5 varies motion and mass per episode)
     base_env = json.loads(json.dumps(envs[0]))
     base_env.pop("quadcopter", None)
@@ -350,6 +354,47 @@ def test_fast_path_equals_exact_path(qt, case):
     np.testing.assert_allclose(fast.state.x.cpu().numpy(), exact.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(fast.state.integ.cpu().numpy(), exact.state.integ.cpu().numpy(), rtol=1e-9,
                                atol=1e-9)
+
+
+@pytest.mark.parametrize("motion", ["linear", "sinusoidal"])
+def test_lqi_gate_threshold_crossings(qt, motion):
+    """LQI with an integral_zero_threshold the tracking error crosses back and
+    forth inside most episodes (the median episode's mean error) and an
+    integral_limit the integral saturates at: the fast step's gate (a step
+    size of dt or 0 on the metric's pre-step ||e_p||, riccati_lqr.py:885-900)
+    takes the exact step's decisions and the oracle's, at every crossing."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = 1024
+    env = {"target": {"motion_type": motion}}
+    base = {"dt": 0.01, "use_lqi": True, "q_int": [1e-2, 1e-2, 1e-1], "integral_limit": 0.3}
+    probe = run_closed_loop(BatchedRiccatiLQR(dict(base, integral_zero_threshold=0.0)), env, n=n,
+                            seeds=np.arange(n)).metrics.cpu().numpy()
+    thr = float(np.median(probe[FIELDS.index("mean_tracking_error")]))
+    ctl_cfg = dict(base, integral_zero_threshold=thr)
+    ctl = BatchedRiccatiLQR(ctl_cfg)
+    fast = run_closed_loop(ctl, env, n=n, seeds=np.arange(n))
+    exact = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), record=True)
+    mf, me = fast.metrics.cpu().numpy(), exact.metrics.cpu().numpy()
+    crossing = (mf[FIELDS.index("max_tracking_error")] > thr) & (mf[FIELDS.index("mean_tracking_error")] < thr)
+    assert crossing.mean() > 0.2
+    for i, f in enumerate(FIELDS):
+        if f in ("overshoot_count", "success", "termination_code", "action_violations", "steps"):
+            np.testing.assert_array_equal(mf[i], me[i], err_msg=f)
+        else:
+            np.testing.assert_allclose(mf[i], me[i], rtol=1e-9, atol=1e-9, err_msg=f)
+    np.testing.assert_allclose(fast.state.integ.cpu().numpy(), exact.state.integ.cpu().numpy(), rtol=1e-9,
+                               atol=1e-9)
+    sample = np.arange(0, n, 8)
+    ep = O.env_params(env)
+    c, K, kc, _, _ = O.controller(ctl_cfg)
+    pat, off = O.draws(motion, sample)
+    x0 = np.array([O.initial_state(ep, ep.motion, pat[i], off[i]) for i in range(len(sample))])
+    om, oxf, ointeg, _ = O.rollout(ep, c, O.criteria(), None, pat, None, None, K, kc, False, x0)
+    np.testing.assert_allclose(mf[:, sample].T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy()[:, sample].T, oxf, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(fast.state.integ[:3].cpu().numpy()[:, sample].T, ointeg, rtol=1e-8, atol=TOL)
 
 
 def test_mixed_motion_order_permutation(qt):

@@ -22,8 +22,10 @@ FIELDS = SCEN["metric_fields"]
 
 # The figure-8 target acceleration is the reference's 1e-6 forward difference
 # of positions (target_motion.py:215-229): it amplifies a 1-ulp sin/cos
-# difference ~1e12x, so any feed-forward run on figure8 agrees only to ~1e-4.
-FF_FIG8_ATOL = 2e-3
+# difference ~1e12x.  The oracle calls sin and cos separately (not glibc's
+# sincos, which rounds differently) and x**2 as libm pow (oracle/Makefile),
+# as numpy does, so its figure-8 targets are bitwise the reference's and the
+# feed-forward scenario needs no exception.
 ATOL = 1e-6
 RTOL = 1e-8
 
@@ -37,7 +39,7 @@ def scenario_episodes(s):
 
 @pytest.mark.parametrize("s", SCEN["scenarios"], ids=[s["name"] for s in SCEN["scenarios"]])
 def test_closed_loop_matches_reference(s):
-    atol = FF_FIG8_ATOL if s["name"] == "ff_figure8" else ATOL
+    atol = ATOL
     for e, seed, env_cfg, ctl_cfg in scenario_episodes(s):
         env = O.env_params(env_cfg)
         c, K, kc, fb, _ = O.controller(ctl_cfg)
@@ -118,9 +120,8 @@ def test_target_states_match_reference():
             pats, _ = O.draws(m, T["seeds"])
             for si in range(len(T["seeds"])):
                 got = np.array([O.target_state(env, mi, pats[si], t) for t in T["times"]])
-                np.testing.assert_allclose(got[:, :6], ref[si][:, :6], rtol=1e-13, atol=1e-12)
-                acc_tol = 1e-3 if m == "figure8" else 1e-12
-                np.testing.assert_allclose(got[:, 6:], ref[si][:, 6:], rtol=1e-9, atol=acc_tol)
+                # bitwise: same libm sin / cos / pow, same operation order
+                np.testing.assert_array_equal(got, ref[si])
 
 
 def test_compute_action_sequences():

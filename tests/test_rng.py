@@ -14,10 +14,35 @@ from conftest import PKG
 import oracle as O
 
 SRC = r"""
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include "qt_rng.hpp"
 int main(int argc, char** argv) {
+  if (argc > 3 && !strcmp(argv[3], "log1p")) {  // restated log1p vs this libm, n arguments in (-1, 3)
+    uint64_t st = strtoull(argv[1], 0, 10) | 1;
+    long bad = 0;
+    const long n = atol(argv[2]);
+    for (long i = 0; i < n; ++i) {
+      st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+      const double u = (double)(st >> 11) * (1.0 / 9007199254740992.0);
+      const double x = (i % 4 == 0) ? -u : (i % 4 == 1) ? -u * 1e-3 : (i % 4 == 2) ? 3.0 * u : -u * u * u * u;
+      const double a = log1p(x), b = qt::fdlibm_log1p(x);
+      if (memcmp(&a, &b, 8)) ++bad;
+    }
+    printf("%ld\n", bad);
+    return 0;
+  }
+  if (argc > 3 && !strcmp(argv[3], "normals")) {  // n normals of one stream, raw doubles to stdout
+    qt::Pcg64 g = qt::pcg64_from_seed(strtoull(argv[1], 0, 10));
+    const long n = atol(argv[2]);
+    for (long i = 0; i < n; ++i) {
+      const double v = qt::pcg_standard_normal(g);
+      fwrite(&v, 8, 1, stdout);
+    }
+    return 0;
+  }
   const unsigned long long seed = strtoull(argv[1], 0, 10);
   const int n = atoi(argv[2]);
   qt::Pcg64 g = qt::pcg64_from_seed(seed);
@@ -46,7 +71,22 @@ def rng_probe(tmp_path_factory):
         nrm = np.array([float.fromhex(v) for v in out[2 * n:]])
         return raw, dbl, nrm
 
+    run.exe = str(exe)
     return run
+
+
+def test_log1p_restatement_matches_libm(rng_probe):
+    # qt::fdlibm_log1p is glibc's s_log1p restated; the ziggurat tail uses it
+    # on host and device so tail normals round as numpy's do
+    out = subprocess.run([rng_probe.exe, "7", "20000000", "log1p"], capture_output=True, text=True, check=True)
+    assert int(out.stdout) == 0
+
+
+def test_normals_million_draws_match_numpy(rng_probe):
+    n = 1_500_000
+    out = subprocess.run([rng_probe.exe, "2024", str(n), "normals"], capture_output=True, check=True).stdout
+    got = np.frombuffer(out, dtype=np.float64)
+    np.testing.assert_array_equal(got, np.random.default_rng(2024).standard_normal(n))
 
 
 @pytest.mark.parametrize("seed", [0, 1, 42, 12345, 2**31 - 1, 2**32, 2**40 + 7, 2**63 - 1])
@@ -69,16 +109,27 @@ def test_device_reset_draws_match_numpy(motion):
     pat, off = seeding.draws(motion, seeds)
     ref_pat, ref_off = O.draws(motion, seeds)
     np.testing.assert_array_equal(off.cpu().numpy().T, ref_off)
-    got = pat.cpu().numpy().T
-    if motion != "linear":
-        np.testing.assert_array_equal(got, ref_pat)
-    else:
-        # normals: bit-exact except the ziggurat's base-strip tail, which goes
-        # through log1p (device libm vs glibc can differ by an ulp): observed
-        # 1 of 80,012 draws, 1 ulp.
-        diff = got != ref_pat
-        assert diff.mean() < 1e-4
-        np.testing.assert_array_max_ulp(got, ref_pat, maxulp=2)
+    # bit-exact, normals included: the ziggurat tail's log1p is glibc's
+    # restated (qt::fdlibm_log1p), not the device libm's
+    np.testing.assert_array_equal(pat.cpu().numpy().T, ref_pat)
+
+
+@pytest.mark.gpu
+def test_device_normals_million_draws_bit_exact():
+    """>= 1M device ziggurat normals (linear reset draws, 3 per seed) bitwise
+    equal to numpy's default_rng(seed).standard_normal(3); the batch holds
+    many base-strip tail draws (the log1p path)."""
+    import sys
+
+    sys.path.insert(0, PKG)
+    from quadtrack.env import seeding
+
+    seeds = np.arange(350_000, dtype=np.int64) * 7919 + 3
+    pat, _ = seeding.draws("linear", seeds)
+    got = pat.cpu().numpy()[:3].T
+    ref = np.stack([np.random.default_rng(int(s)).standard_normal(3) for s in seeds])
+    assert got.size >= 1_000_000
+    np.testing.assert_array_equal(got, ref)
 
 
 @pytest.mark.gpu
@@ -94,5 +145,5 @@ def test_device_reset_draws_mixed_motion():
     for m in range(5):
         idx = np.nonzero(motion == m)[0]
         rp, ro = O.draws(m, idx + 10**9)
-        np.testing.assert_array_max_ulp(pat.cpu().numpy().T[idx], rp, maxulp=2)
+        np.testing.assert_array_equal(pat.cpu().numpy().T[idx], rp)
         np.testing.assert_array_equal(off.cpu().numpy().T[idx], ro)
