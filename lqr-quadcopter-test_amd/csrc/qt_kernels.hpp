@@ -452,6 +452,8 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   const VelLin lin = UNI ? k.vl : make_vel_lin(e, pl_lane);
   const double R = cr.target_radius, eR = e.target_radius;
   const double vm2 = e.max_velocity * e.max_velocity * (1.0 - 1e-14);
+  // position bounds |p|_inf > max_position as a >= test (the vote's one compare)
+  const double pos_up = nextafter(e.max_position, INFINITY);
   const int W = cr.overshoot_window;
   // Launch start: the pre-step tracking error of the current observation,
   // roll / pitch trig, target rotor, overshoot counter.  The observation is
@@ -528,17 +530,18 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       // step's pre-step error (positions are not constrained)
       err = sqrt_pos(sq3_ref(x[0] - tg.p[0], x[1] - tg.p[1], x[2] - tg.p[2]));
       on_post += err <= eR;
-      const bool vbad = !(x[3] * x[3] + x[4] * x[4] + x[5] * x[5] < vm2);
+      // the stop conditions as one maximum >= 0 (the state is finite): speed
+      // at the clamp's guard band, position bounds, time limit, end of the run
+      // (rem, uniform) — one compare and one ballot straight into the branch,
+      // no serial scalar chain at the end of the step
+      --rem;
+      const double stop_m =
+          fmax(fmax(fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) - pos_up, (x[3] * x[3] + x[4] * x[4] + x[5] * x[5]) - vm2),
+               fmax(t - e.max_episode_time, -(double)rem));
       if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
       double ap[2] = {a0[0], a0[1]};
       attitude_trig_advance(x + 6, ap, ta, rk);
-      const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
-      const bool tl = t >= e.max_episode_time;
-      --rem;
-      // one vote: each compare's lane mask and the run's end, or-ed on the scalar unit
-      const uint64_t stop = __builtin_amdgcn_ballot_w64(vbad) | __builtin_amdgcn_ballot_w64(pb) |
-                            __builtin_amdgcn_ballot_w64(tl) | (rem == 0 ? ~0ull : 0ull);
-      if (stop) break;
+      if (__builtin_amdgcn_ballot_w64(stop_m >= 0.0)) break;
     } while (true);
     const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;
     s += ran;
