@@ -484,6 +484,11 @@ struct LaunchConst {
   Plant pl;
   double rc[5][3], rs[5][3];  // per motion type: cos / sin of fl(omega_i dt)
   double om[5][3];            // per motion type: omega_i
+  // deferred-wave flag of this launch set (per stream, qt_rollout.hip): a
+  // fast-flavour wave that leaves its episodes to the exact pass writes
+  // `epoch` there; the exact pass returns at once unless it reads its epoch
+  unsigned long long* defer_flag;
+  unsigned long long epoch;
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)

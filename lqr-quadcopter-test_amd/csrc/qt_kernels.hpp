@@ -618,7 +618,10 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
               fabs(x[9]) <= c.max_rate && fabs(x[10]) <= c.max_rate;
   const bool wave_ok = __builtin_amdgcn_ballot_w64(!lane_ok) == 0;
   if (FLAVOR != kExact) {
-    if (!wave_ok) return;
+    if (!wave_ok) {
+      if (lc.defer_flag) *lc.defer_flag = lc.epoch;  // the exact pass has work (every lane stores the same value)
+      return;
+    }
 #if QT_CLOCK_STAMP && defined(QT_FAST_TU)
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -671,6 +674,9 @@ template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
+  // the exact pass after a fast flavour that deferred no wave: nothing to do
+  // (one uniform load per wave instead of the wave test's ~40 per lane)
+  if (FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch) return;
   const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
   if (slot < 0) return;
   rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);

@@ -8,7 +8,10 @@
 // instantiated in qt_rollout_fast.hip.
 // Reference functions: src/quadcopter_tracking/... of the reference repo.
 #include "qt_kernels.hpp"
+#include <atomic>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 using namespace qtk;
 
@@ -380,8 +383,31 @@ struct ExactLaunch {
   }
 };
 
-// One rollout launch set: the fast flavour the launch-level preconditions
-// allow, then the exact kernel for the waves it left (or for everything).
+// Deferred-wave flags, one device word per (device, stream): launches on one
+// stream run in order, so a launch set's exact pass reads the word its own
+// fast kernel wrote (or an older epoch: no deferred wave).  Epochs are unique
+// per process, so a stale word never matches.  Allocated once per stream and
+// kept for the process lifetime (8 bytes each).
+std::atomic<unsigned long long> g_defer_epoch{0};
+
+unsigned long long* defer_flag_for(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned long long*> flags;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = flags.find({dev, s});
+  if (it != flags.end()) return it->second;
+  unsigned long long* f = nullptr;
+  if (hipMalloc(&f, sizeof(*f)) != hipSuccess) return nullptr;
+  if (hipMemset(f, 0, sizeof(*f)) != hipSuccess) {  // epoch 0 is never issued
+    (void)hipFree(f);
+    return nullptr;
+  }
+  flags[{dev, s}] = f;
+  return f;
+}
+
 // The step flavour a launch can take (launch-level preconditions).
 int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
@@ -396,11 +422,13 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                    double* rec, bool grouped = false) {
-  const LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
+  LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
   const int flavor = flavor_for(kc, ks, no_yaw, e, c, rec);
   if (flavor != kExact) {
+    lc.defer_flag = defer_flag_for(s);  // null (no flag: the exact pass tests every wave) if unavailable
+    lc.epoch = g_defer_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
     launch_fast(flavor, uni, grouped, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
   }

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--config", type=int, required=True)
     ap.add_argument("--episodes", type=int, default=None)
     ap.add_argument("--repeat", type=int, default=3)
+    ap.add_argument("--warmup-s", type=float, default=1.0,
+                    help="untimed back-to-back rollouts first (the clock ramps up over ~1 s of load)")
     ap.add_argument("--no-group", action="store_true", help="config 5: one runtime-motion launch instead of groups")
     args = ap.parse_args()
 
@@ -66,6 +68,11 @@ def main():
     nsteps = max_steps_for(env)
     stream = torch.cuda.current_stream(dev)
     times = []
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < args.warmup_s:
+        core.reset(env, batch, st)
+        core.rollout(env, sh.controller.ctrl, crit, batch, st, nsteps)
+        torch.cuda.synchronize()
     for _ in range(args.repeat):
         core.reset(env, batch, st)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -93,7 +100,8 @@ def main():
             "setup_s": {"controller_dare_and_params": round(t_ctl, 4), "batch_draws": round(t_batch, 4)},
             "dare_max_iterations": int(sh.controller.iters.max().item()),
             "dare_fallbacks": int((sh.controller.status != 0).sum().item()),
-            "rollout_ms": round(kern, 3), "rollout_ms_all": [round(t, 3) for t in times],
+            "rollout_ms": round(kern, 3), "rollout_ms_median": round(sorted(times)[len(times) // 2], 3),
+            "warmup_s": args.warmup_s, "rollout_ms_all": [round(t, 3) for t in times],
             "env_steps": float(steps.item()), "env_steps_per_s": round(float(steps.item()) / (kern * 1e-3), 1),
             "summary": {"mean_on_target_ratio": s.mean_on_target_ratio, "std_on_target_ratio": s.std_on_target_ratio,
                         "mean_tracking_error": s.mean_tracking_error, "std_tracking_error": s.std_tracking_error,

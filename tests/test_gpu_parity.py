@@ -397,6 +397,42 @@ def test_lqi_gate_threshold_crossings(qt, motion):
     np.testing.assert_allclose(fast.state.integ[:3].cpu().numpy()[:, sample].T, ointeg, rtol=1e-8, atol=TOL)
 
 
+def test_deferred_waves_run_exact_pass(qt):
+    """Waves that fail the fast flavour's wave test (here: roll beyond the
+    tilt clamp at the launch start) are left to the exact pass, which runs
+    only when its launch set's fast kernel flagged a deferral (per-stream
+    epoch flag).  Launch 1 defers one wave; launch 2 (same stream, the tilt
+    now clamped) defers none, so its exact pass must skip on the stale flag.
+    Both against the exact step everywhere (recording forces it)."""
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.env.config import EnvConfig
+    from quadtrack.rollout import build_batch
+
+    n = 512
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    cfg = EnvConfig.from_dict({"target": {"motion_type": "circular"}})
+    env = cfg.to_params()
+    crit = core.criteria()
+    out = []
+    for record in (False, True):
+        batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+        st = core.RolloutState.empty(n, batch.device)
+        core.reset(env, batch, st)
+        st.x[6, 192:256] = 1.2  # wave 3: outside the +-pi/3 tilt clamp
+        st.x[7, 200:210] = -1.3
+        for k in (150, 150, 2700):
+            rec = torch.full((k, 16, n), float("nan"), dtype=torch.float64, device=batch.device) if record else None
+            core.rollout(env, ctl.ctrl, crit, batch, st, k, rec)
+        out.append((core.episode_metrics(crit, st).cpu().numpy(), st.x.cpu().numpy()))
+    (mf, xf), (me, xe) = out
+    steps = FIELDS.index("steps")
+    np.testing.assert_array_equal(mf[steps], me[steps])
+    assert np.all(mf[steps] == 3000)
+    np.testing.assert_allclose(mf, me, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(xf, xe, rtol=1e-9, atol=1e-9)
+
+
 def test_mixed_motion_order_permutation(qt):
     """Mixed motion types: the per-step runtime-motion kernel, the same kernel
     under a permuting `order`, and the grouped motion-specialised launches
