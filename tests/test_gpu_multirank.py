@@ -65,3 +65,44 @@ def test_two_rank_summary_equals_single():
               "mean_control_effort"):
         assert got[k] == pytest.approx(ref[k], rel=1e-12, abs=1e-15), k
     assert np.isfinite(got["mean_tracking_error"])
+
+
+def _rccl_rank(port, q):
+    """One rank over RCCL (backend "nccl") on the box's GPU: the summary's
+    device all-reduces and all-gather run through RCCL itself."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "lqr-quadcopter-test_amd"))
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from quadtrack import evaluate_batched
+
+        assert dist.get_backend() == "nccl"
+        s = evaluate_batched({"dt": 0.01}, CFG, num_episodes=N, base_seed=0, with_episode_metrics=False)
+        q.put(s.to_dict())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_single_rank_summary_equals_local():
+    """The RCCL code path of the metric reduction (one rank: a full RCCL
+    communicator on the GPU, collectives on device tensors) gives the
+    single-process summary; multi-GPU runs use the same calls."""
+    from quadtrack import evaluate_batched
+
+    ref = evaluate_batched({"dt": 0.01}, CFG, num_episodes=N, base_seed=0, with_episode_metrics=False).to_dict()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rank, args=(_port(), q))
+    p.start()
+    got = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for k, v in ref.items():
+        np.testing.assert_allclose(got[k], v, rtol=1e-12, atol=1e-12, err_msg=k)
