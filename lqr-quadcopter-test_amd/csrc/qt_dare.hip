@@ -386,6 +386,24 @@ __device__ bool check_sym_eigs(int n, const double* M, double* scratch, bool str
 
 constexpr int kMaxN = 16, kMaxP = 8;
 
+// Dynamic LDS layout of dare_dense_kernel (doubles): sA, sA0, sG, sH, sT2,
+// sQ (n x n); sW (n x n | p x p systems); sY (n x 2n | p x n right-hand
+// sides); sT (n x n | p x n products | the p x p eigen scratch); sB (n x p);
+// sR (p x p).
+struct DenseLds {
+  int nn, w, y, t;
+  __host__ __device__ DenseLds(int n, int p) {
+    nn = n * n;
+    w = nn > p * p ? nn : p * p;
+    y = 2 * nn > p * n ? 2 * nn : p * n;
+    t = nn > p * n ? nn : p * n;
+    t = t > p * p ? t : p * p;
+  }
+  __host__ __device__ int doubles(int n, int p) const { return 6 * nn + w + y + t + n * p + p * p; }
+};
+
+inline size_t dense_lds_bytes(int n, int p) { return sizeof(double) * (size_t)DenseLds(n, p).doubles(n, p); }
+
 // General dense SDA, one wavefront per problem.  Hover model (A, B == NULL):
 // A, B built from (dt, mass, gravity) exactly as build_linearized_system /
 // build_augmented_lqi_system; otherwise A [n*n] and B [n*p] are read (shared
@@ -402,9 +420,21 @@ __global__ __launch_bounds__(kDenseThreads) void dare_dense_kernel(int n, int p,
                                                                    int32_t* iters) {
   const int64_t pb = blockIdx.x;
   if (pb >= m) return;
-  __shared__ double sA[kMaxN * kMaxN], sA0[kMaxN * kMaxN], sB[kMaxN * kMaxP], sG[kMaxN * kMaxN],
-      sH[kMaxN * kMaxN], sW[kMaxN * kMaxN], sY[2 * kMaxN * kMaxN], sT[kMaxN * kMaxN], sT2[kMaxN * kMaxN],
-      sR[kMaxP * kMaxP], sQ[kMaxN * kMaxN];
+  // LDS sized to the problem (dense_lds_bytes): ~7 KB at n = 9, p = 4, so
+  // ~20 problems share a CU instead of the 6 that fixed 16 x 16 arrays allowed
+  extern __shared__ double smem[];
+  const DenseLds L(n, p);
+  double* sA = smem;
+  double* sA0 = sA + L.nn;
+  double* sB = sA0 + L.nn;
+  double* sG = sB + n * p;
+  double* sH = sG + L.nn;
+  double* sW = sH + L.nn;
+  double* sY = sW + L.w;
+  double* sT = sY + L.y;
+  double* sT2 = sT + L.t;
+  double* sR = sT2 + L.nn;
+  double* sQ = sR + p * p;
   __shared__ int sh_i[2];
   const int tid = threadIdx.x;
   const bool hover = Ain == nullptr;
@@ -599,7 +629,7 @@ extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gra
       dare_axis_kernel<6><<<grid, 256, 0, s>>>(m, dt, gravity, mass, q, r, K, P, status, iters);
   } else {
     if (m > 0x7fffffff) return QT_EINVAL;
-    dare_dense_kernel<<<(int)m, kDenseThreads, 0, s>>>(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r,
+    dare_dense_kernel<<<(int)m, kDenseThreads, dense_lds_bytes(n_state, 4), s>>>(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r,
                                                        1, K, P, status, iters);
   }
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
@@ -611,7 +641,7 @@ extern "C" int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, c
   if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > 0x7fffffff) return QT_EINVAL;
   if (m == 0) return QT_OK;  // empty: no pointer is read
   if (!A || !B || !q || !r || !K || !status) return QT_EINVAL;
-  dare_dense_kernel<<<(int)m, kDenseThreads, 0, (hipStream_t)stream>>>(n, p, m, A, B, ab_per_problem, 0.0, 0.0,
+  dare_dense_kernel<<<(int)m, kDenseThreads, dense_lds_bytes(n, p), (hipStream_t)stream>>>(n, p, m, A, B, ab_per_problem, 0.0, 0.0,
                                                                        nullptr, q, r, 0, K, P, status, iters);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }
