@@ -409,9 +409,11 @@ __device__ __forceinline__ void derivatives(const qt_env_params& e, const Plant&
 // Rates / attitudes (uniform: launch constants, computed on the host and
 // passed as a kernel argument, so they live in SGPRs):
 // w_new = wy w + wu u, a_new = a + ay w + au u, stage attitude offsets
-// d2 = h2 w, d3 = d3y w + d3u u, d4 = d4y w + d4u u.
+// d2 = h2 w, d3 = d3y w + d3u u, d4 = d4y w + d4u u, and the third stage's
+// offset relative to the second, e3 = d3 - d2 = e3y w + d3u u (|e3| is
+// O(dt^2): the stage rates differ by h/2 times the rate derivative).
 struct RateLin {
-  double wy, wu, ay, au, h2, d3y, d3u, d4y, d4u;
+  double wy, wu, ay, au, h2, d3y, d3u, d4y, d4u, e3y;
 };
 
 // Velocities / positions (per lane: delta depends on the episode's mass):
@@ -441,6 +443,7 @@ QT_HD RateLin make_rate_lin(const qt_env_params& e) {
   double o[5];
   rk4_linear(lam, h, 1.0, zero, o);
   L.wy = o[3], L.ay = o[4], L.d3y = 0.5 * h * o[0], L.d4y = h * o[1];
+  L.e3y = 0.5 * h * (o[0] - 1.0);  // o[0] = 1 - h lam / 2 in [1/2, 1]: the difference is exact
   rk4_linear(lam, h, 0.0, ten, o);
   L.wu = o[3], L.au = o[4], L.d3u = 0.5 * h * o[0], L.d4u = h * o[1];
   L.h2 = 0.5 * h;
@@ -528,51 +531,65 @@ inline LaunchConst make_launch_const(const qt_env_params& e) {
   return k;
 }
 
-// Roll / pitch sin / cos carried across yaw-at-rest fast steps: the new
-// attitude differs from the step start's by |d| <= dt * max_rate (+ the
-// wrap's rounding; the tilt clamp only shortens it; rate_bounded_ok), so the
-// carried values are rotated by the exact difference of the rounded angles
-// with rate_sincos (angle addition): they follow sin / cos of the angles the
-// reference evaluates with a drift of a few ulp per step.
-__device__ __forceinline__ void attitude_trig_advance(const double* a_new, double* a_prev, Trig& ta,
-                                                      const RateCoef& rk = RateCoef{}) {
+// Roll / pitch sin / cos carried across yaw-at-rest fast steps.  The new
+// attitude differs from the fourth RK4 stage's by a residual of O(dt^3)
+// (attitude_residual_bound), so the carried values are the stage-4 trig
+// (integrate_yaw0's t4) rotated by r = (a_new - a0) - d4, the exact
+// difference of the rounded angles less the stage-4 offset, with tiny_sincos:
+// they follow sin / cos of the angles the reference evaluates with a drift of
+// a few ulp per step.  Taken before the tilt clamp (the bound holds for the
+// unclamped update), which run_yaw0 then applies to the trig as well.
+__device__ __forceinline__ void attitude_trig_resid(const double* a_new, const double* a0, const double* d4,
+                                                    const Trig& t4, Trig& ta) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    double sd, cd;
-    rate_sincos(a_new[i] - a_prev[i], &sd, &cd, rk);
-    const double s0 = ta.s[i], c0 = ta.c[i];
-    ta.s[i] = fma(s0, cd, c0 * sd);
-    ta.c[i] = fma(c0, cd, -(s0 * sd));
-    a_prev[i] = a_new[i];
+    double sd, cm;
+    tiny_sincos((a_new[i] - a0[i]) - d4[i], &sd, &cm);
+    rotate_cm(t4.s[i], t4.c[i], sd, cm, &ta.s[i], &ta.c[i]);
   }
 }
 
 // One yaw-at-rest RK4 step in closed form (RateLin, VelLin); x[8], x[11] untouched.
 // ta: sin / cos of roll and pitch at the step start (carried by the caller).
+// Out: the stage-4 attitude offsets d4 and their trig t4 (attitude_trig_resid).
 __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L, const Plant& pl, const Trig& ta,
-                                               double* x, const double* u, const RateCoef& rk = RateCoef{}) {
+                                               double* x, const double* u, const RateCoef& rk, double* d4,
+                                               Trig& t4) {
   const double w0 = x[9], w1 = x[10];
   Trig t[4];
   t[0] = ta;
   const double d2[3] = {R.h2 * w0, R.h2 * w1, 0.0};
-  const double d3[3] = {fma(R.d3y, w0, R.d3u * u[1]), fma(R.d3y, w1, R.d3u * u[2]), 0.0};
-  const double d4[3] = {fma(R.d4y, w0, R.d4u * u[1]), fma(R.d4y, w1, R.d4u * u[2]), 0.0};
+  d4[0] = fma(R.d4y, w0, R.d4u * u[1]);
+  d4[1] = fma(R.d4y, w1, R.d4u * u[2]);
+  const double d4v[3] = {d4[0], d4[1], 0.0};
   trig_shift<true, true>(x + 6, t[0], d2, t[1], rk);
-  trig_shift<true, true>(x + 6, t[0], d3, t[2], rk);
-  trig_shift<true, true>(x + 6, t[0], d4, t[3], rk);
+  // stage 3 from stage 2 by e3 = d3 - d2, |e3| <= kStage3Angle (rate_bounded_ok)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double e3 = fma(R.e3y, x[9 + i], R.d3u * u[1 + i]);
+    double sd, cm;
+    resid_sincos(e3, &sd, &cm, rk);
+    rotate_cm(t[1].s[i], t[1].c[i], sd, cm, &t[2].s[i], &t[2].c[i]);
+  }
+  trig_shift<true, true>(x + 6, t[0], d4v, t[3], rk);
+  t4 = t[3];
   // thrust direction R3 at each stage (derivatives<true>): (sin th cos phi, -sin phi, cos th cos phi)
   double sv[3] = {0.0, 0.0, 0.0}, sp[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 3; ++i) {
     const double r0 = t[i].s[1] * t[i].c[0], r1 = -t[i].s[0], r2 = t[i].c[1] * t[i].c[0];
     sv[0] = fma(L.wv[i], r0, sv[0]);
     sv[1] = fma(L.wv[i], r1, sv[1]);
     sv[2] = fma(L.wv[i], r2, sv[2]);
-    if (i < 3) {
-      sp[0] = fma(L.pa[i], r0, sp[0]);
-      sp[1] = fma(L.pa[i], r1, sp[1]);
-      sp[2] = fma(L.pa[i], r2, sp[2]);
-    }
+    sp[0] = fma(L.pa[i], r0, sp[0]);
+    sp[1] = fma(L.pa[i], r1, sp[1]);
+    sp[2] = fma(L.pa[i], r2, sp[2]);
+  }
+  {  // stage 4 reaches the velocities only: its weight folded into cos phi
+    const double wc = L.wv[3] * t[3].c[0];
+    sv[0] = fma(wc, t[3].s[1], sv[0]);
+    sv[1] = fma(L.wv[3], -t[3].s[0], sv[1]);
+    sv[2] = fma(wc, t[3].c[1], sv[2]);
   }
   const double tm = u[0] * pl.inv_mass;
 #pragma unroll
@@ -774,9 +791,26 @@ __host__ __device__ inline bool fast_path_ok(const qt_env_params& e, const qt_ct
 // attitude offset h * w (h <= dt) is then at most dt * max_rate <= kRateAngle,
 // and with max_rate below max_angular_velocity the env's angular-velocity
 // clamp (quadcopter_env.py:446-450) never acts (constrain_fast_apply<true>).
+// The residuals of the yaw-at-rest step's trig (integrate_yaw0,
+// attitude_trig_resid) follow from the same linear rate dynamics: with
+// k1 = 10 u - lam w (lam = 10 + c, |k1| <= (10 + lam) max_rate) the third
+// stage's offset exceeds the second's by e3 = (h/2)(h/2) k1, and the step's
+// attitude update h/6 (y1 + 2 y2 + 2 y3 + y4) exceeds the fourth stage's
+// offset h y3 by h/6 (y1 + 2 y2 - 4 y3 + y4) = h^3 lam (1 + lam h / 2) k1 / 12.
+// At the defaults (dt 0.01, max_rate 3): 1.5e-3 and 5.3e-5.
+__host__ __device__ inline double stage3_residual_bound(const qt_env_params& e, const qt_ctrl_params& c) {
+  const double lam = 10.0 + e.drag_angular, k1 = (10.0 + lam) * c.max_rate;
+  return 0.25 * e.dt * e.dt * k1 * (1.0 + 1e-6);
+}
+__host__ __device__ inline double attitude_residual_bound(const qt_env_params& e, const qt_ctrl_params& c) {
+  const double lam = 10.0 + e.drag_angular, h = e.dt, k1 = (10.0 + lam) * c.max_rate;
+  return h * h * h * lam * (1.0 + 0.5 * lam * h) / 12.0 * k1 * (1.0 + 1e-6) + 1e-15;  // + the wrap's rounding
+}
+
 __host__ __device__ inline bool rate_bounded_ok(const qt_env_params& e, const qt_ctrl_params& c) {
   return c.max_rate >= 0.0 && e.drag_angular >= 0.0 && e.dt > 0.0 && e.dt * (10.0 + e.drag_angular) <= 1.0 &&
-         e.dt * c.max_rate * (1.0 + 1e-9) <= kRateAngle && c.max_rate * (1.0 + 1e-9) <= e.max_angular_velocity;
+         e.dt * c.max_rate * (1.0 + 1e-9) <= kRateAngle && c.max_rate * (1.0 + 1e-9) <= e.max_angular_velocity &&
+         stage3_residual_bound(e, c) <= kStage3Angle && attitude_residual_bound(e, c) <= kAdvanceAngle;
 }
 
 // Fast-path state constraints: the common case of _apply_state_constraints
@@ -817,8 +851,11 @@ __device__ __forceinline__ void constrain_fast_apply(const qt_env_params& e, dou
     const double adj = YAW0 ? 0.0 : (b < 0.0 ? kTwoPi : (b >= kTwoPi ? -kTwoPi : 0.0));
     x[6 + i] = YAW0 ? b - kPi : (b + adj) - kPi;
   }
-  x[6] = clip_num(x[6], -kMaxTilt, kMaxTilt);
-  x[7] = clip_num(x[7], -kMaxTilt, kMaxTilt);
+  // YAW0: the tilt clamp is the caller's (run_yaw0's tilt_clamp, after the carried trig)
+  if (!YAW0) {
+    x[6] = clip_num(x[6], -kMaxTilt, kMaxTilt);
+    x[7] = clip_num(x[7], -kMaxTilt, kMaxTilt);
+  }
 }
 
 // _check_termination without branches, for the fast step.  Its state stays

@@ -170,12 +170,12 @@ __device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int
 // takes the exact step's decisions; rare lanes/steps (speed at the
 // clamp, attitude far outside [-pi, pi), tracking error at the radius within
 // 1e-14) fall back to the exact constraint / comparison code inside the step.
-template <bool FAST, bool YAW0, int MOTION, int KC, bool FF, bool KS>
+template <bool FAST, int MOTION, int KC, bool FF, bool KS>
 __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
                                           const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
                                           Target& tg, double& t, Acc& a, int nsteps, double* __restrict__ rec,
-                                          int64_t n, int64_t ep, const RateLin& rl) {
+                                          int64_t n, int64_t ep) {
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
@@ -190,16 +190,6 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
   if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
-  // yaw-at-rest fast steps: RK4 in closed form (integrate_yaw0)
-  // and carried roll / pitch sin / cos (attitude_trig_advance)
-  VelLin lin;
-  Trig ta;
-  double aprev[2];
-  if constexpr (FAST && YAW0) {
-    lin = make_vel_lin(e, pl);
-    trig_of<true>(x + 6, ta);
-    aprev[0] = x[6], aprev[1] = x[7];
-  }
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -240,10 +230,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     // ---- env.step (quadcopter_env.py:152-232)
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
-      if constexpr (YAW0)
-        integrate_yaw0(rl, lin, pl, ta, x, u);
-      else
-        integrate<true, false>(e, pl, x, u);
+      integrate<true, false>(e, pl, x, u);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kCarry)
@@ -254,22 +241,17 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       const double se = q0 * q0 + q1 * q1 + q2 * q2;  // positions are not constrained
       se_pre = se;
-      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<YAW0>(e, x));
+      const bool ok = ((se < er2lo) | (se > er2hi)) & ((QT_ABLATE & QT_ABL_CONSTRAIN) || constrain_fast_ok<false>(e, x));
       // Wave-uniform choice: when any lane is off the fast preconditions the
       // whole wave runs the exact code, which takes the fast code's decisions
       // on the lanes that qualify.  A uniform, expected condition is a
       // not-taken scalar branch with the exact code out of line; a divergent
       // if / else cost a taken branch around the else block every step.
       if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
-        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<YAW0>(e, x);
-        if constexpr (YAW0) attitude_trig_advance(x + 6, aprev, ta);
+        if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<false>(e, x);
         a.on_post += se < er2lo;
       } else {  // rare: exact constraints and comparison
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
-        if constexpr (YAW0) {  // restart the carried attitude trig (|roll|, |pitch| <= pi/3 again)
-          trig_of<true>(x + 6, ta);
-          aprev[0] = x[6], aprev[1] = x[7];
-        }
         a.on_post += norm_le(se, e.target_radius);
       }
       if (QT_ABLATE & QT_ABL_TERMINATION)
@@ -427,6 +409,24 @@ __device__ __forceinline__ void clamp_velocity(const qt_env_params& e, double* x
   }
 }
 
+// The tilt clamp (quadcopter_env.py:460-463) on roll / pitch and on their
+// carried sin / cos: sin is increasing and cos decreasing in |a| on the fast
+// step's range (|a| <= pi/3 + kRateAngle < pi/2), so
+// sin(clip(a)) = clip(sin a, -sin(pi/3), sin(pi/3)) and
+// cos(clip(a)) = max(cos a, cos(pi/3)), with the bounds as sincos_tilt gives
+// them (trig_of of a clamped angle).  Near the clamp a rounding of sin a or
+// cos a to the bound moves it by <= 1 ulp.
+__device__ __forceinline__ void tilt_clamp(double* x, Trig& ta) {
+  double sm, cm;
+  sincos_tilt(kMaxTilt, &sm, &cm);  // folded at compile time
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    x[6 + i] = clip_num(x[6 + i], -kMaxTilt, kMaxTilt);
+    ta.s[i] = clip_num(ta.s[i], -sm, sm);
+    ta.c[i] = fmax(ta.c[i], cm);
+  }
+}
+
 // The yaw-at-rest fast loop (flavour kYaw0).  One wave-uniform loop: every
 // step runs branch-free (closed-form RK4, carried roll / pitch and target
 // trig, fused metrics) and ends with ONE wave vote; the loop leaves only when
@@ -479,6 +479,12 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   double cur = a.os_cur;
   int on_pre = a.on_pre, on_post = a.on_post, os_count = a.os_count;
   bool stepped = false;
+  // Where the tilt clamp goes (the same arithmetic either way): LQI runs can
+  // diverge and hold their tilt at the clamp, so their loop
+  // applies it every step; the others stop the loop at a clamping step (rare
+  // for them) and apply it after, which spares the loop its ~10 operations.
+  constexpr bool kTiltVote = KC != 9;
+  const double tilt_up = nextafter(kMaxTilt, INFINITY);  // |a| > kMaxTilt as a >= test
   int s = 0;
   while (a.term == QT_TERM_RUNNING && s < nsteps) {
     const int s0 = s;
@@ -486,7 +492,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
     RateCoef rk;
     do {
       rk.pin();
-      const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_advance)
+      const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_resid)
       // ---- compute_action on the current observation (riccati_lqr.py:779-967)
       double u[4];
       if (QT_ABLATE & QT_ABL_CONTROLLER) {
@@ -513,7 +519,9 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       }
       // ---- env.step (quadcopter_env.py:152-232): the command is finite and
       // inside the env clamps, so parsing is the identity
-      integrate_yaw0(k.rl, lin, pl, ta, x, u, rk);
+      double d4[2];
+      Trig t4;
+      integrate_yaw0(k.rl, lin, pl, ta, x, u, rk, d4, t4);
       const double t0 = t;
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
@@ -530,17 +538,23 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       // step's pre-step error (positions are not constrained)
       err = sqrt_pos(sq3_ref(x[0] - tg.p[0], x[1] - tg.p[1], x[2] - tg.p[2]));
       on_post += err <= eR;
+      // angle wrap (no correction: tilt-bounded), carried roll / pitch trig of
+      // the wrapped angles (attitude_trig_resid's bound holds for them), then
+      // the tilt clamp on both the angles and their trig (tilt_clamp): here,
+      // or after the loop, which a tilt beyond the clamp then stops (kTiltVote)
+      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
+      attitude_trig_resid(x + 6, a0, d4, t4, ta);
+      if (!kTiltVote && !(QT_ABLATE & QT_ABL_CONSTRAIN)) tilt_clamp(x, ta);
       // the stop conditions as one maximum >= 0 (the state is finite): speed
       // at the clamp's guard band, position bounds, time limit, end of the run
-      // (rem, uniform) — one compare and one ballot straight into the branch,
-      // no serial scalar chain at the end of the step
+      // (rem, uniform), kTiltVote: tilt beyond its clamp — one compare and one
+      // ballot straight into the branch, no serial scalar chain at the end of
+      // the step
       --rem;
-      const double stop_m =
+      double stop_m =
           fmax(fmax(fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) - pos_up, (x[3] * x[3] + x[4] * x[4] + x[5] * x[5]) - vm2),
                fmax(t - e.max_episode_time, -(double)rem));
-      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
-      double ap[2] = {a0[0], a0[1]};
-      attitude_trig_advance(x + 6, ap, ta, rk);
+      if (kTiltVote) stop_m = fmax(stop_m, fmax(fabs(x[6]), fabs(x[7])) - tilt_up);
       if (__builtin_amdgcn_ballot_w64(stop_m >= 0.0)) break;
     } while (true);
     const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;
@@ -548,9 +562,13 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
     a.steps += ran;
     stepped = true;
     z = z <= 0 ? kNeg : z;  // off phase: keep z far below 1 for the next run
-    // finish the last step exactly: the velocity clamp where it acts, per-lane
-    // termination (both no-ops for a lane the vote did not stop)
-    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) clamp_velocity(e, x);
+    // finish the last step exactly: the velocity and (kTiltVote) tilt clamps
+    // where they act, per-lane termination (all no-ops for a lane the vote did
+    // not stop)
+    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) {
+      clamp_velocity(e, x);
+      if (kTiltVote && (fabs(x[6]) > kMaxTilt || fabs(x[7]) > kMaxTilt)) tilt_clamp(x, ta);
+    }
     a.term = (QT_ABLATE & QT_ABL_TERMINATION) ? (t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING)
                                                : termination_fast(e, t, x);
   }
@@ -628,8 +646,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     if constexpr (FLAVOR == kYaw0)
       run_yaw0<MOTION, KC, FF, KS, UNI>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, lc);
     else
-      run_steps<true, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
-                                                 rec, n, ep, lc.rl);
+      run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec,
+                                          n, ep);
 #if QT_CLOCK_STAMP && defined(QT_FAST_TU)
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
@@ -643,8 +661,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
 #endif
   } else {
     if (deferred != kExact && wave_ok) return;
-    run_steps<false, false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
-                                                rec, n, ep, lc.rl);
+    run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec, n,
+                                         ep);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
   // feed-forward reads them); the stored observation carries the reference's

@@ -123,10 +123,11 @@ constexpr double kRateAngle = 0.031;
 struct RateCoef {
   double s7 = -1.9841269841269841e-04;  // -1/7!
   double c6 = -1.3888888888888889e-03;  // -1/6!
+  double s5 = 8.3333333333333332e-03;   // 1/5! (resid_sincos)
 #if defined(__HIP_DEVICE_COMPILE__)
   // opaque to the optimiser: kept in VGPRs across a loop instead of being
   // re-materialised from scalar registers each trip (no instruction emitted)
-  __device__ __forceinline__ void pin() { asm("" : "+v"(s7), "+v"(c6)); }
+  __device__ __forceinline__ void pin() { asm("" : "+v"(s7), "+v"(c6), "+v"(s5)); }
 #else
   void pin() {}
 #endif
@@ -140,6 +141,38 @@ QT_HD void rate_sincos(double d, double* s, double* c, const RateCoef& k = RateC
   double q = fma(z, k.c6, 4.1666666666666664e-02);  // 1/4!
   q = fma(z, q, -0.5);
   *c = fma(z, q, 1.0);
+}
+
+// sin d and cos d - 1 of the residual between two nearby RK4 stage offsets
+// (the yaw-at-rest step's third stage relative to its second),
+// |d| <= kStage3Angle: Taylor polynomials to d^5 / d^4, truncation below
+// 3e-21 (sin) and 5.7e-18 (cos - 1, the d^6 / 6! term).  The rotation takes
+// cos d - 1 (rotate_cm), so that no digit of the small correction is lost to
+// the rounding of cos d near 1.
+constexpr double kStage3Angle = 4e-3;
+
+QT_HD void resid_sincos(double d, double* s, double* cm, const RateCoef& k = RateCoef{}) {
+  const double z = d * d;
+  const double p = fma(z, k.s5, -1.6666666666666666e-01);  // -1/3!
+  *s = fma(d * z, p, d);
+  const double q = fma(z, 4.1666666666666664e-02, -0.5);  // 1/4!, -1/2!
+  *cm = z * q;
+}
+
+// sin d and cos d - 1 of a tiny angle, |d| <= kAdvanceAngle: d - d^3 / 6 and
+// -d^2 / 2, truncation below 3e-22 (sin) and 4.2e-18 (cos - 1).
+constexpr double kAdvanceAngle = 1e-4;
+
+QT_HD void tiny_sincos(double d, double* s, double* cm) {
+  *cm = d * (-0.5 * d);
+  *s = fma(d * *cm, 3.3333333333333331e-01, d);  // d + d (-d^2 / 2) / 3
+}
+
+// (s, c) rotated by the angle whose sine is sd and cosine 1 + cm:
+// s' = s + (s cm + c sd), c' = c + (c cm - s sd)
+QT_HD void rotate_cm(double s0, double c0, double sd, double cm, double* s, double* c) {
+  *s = fma(c0, sd, fma(s0, cm, s0));
+  *c = fma(-s0, sd, fma(c0, cm, c0));
 }
 
 #if defined(__HIPCC__)

@@ -30,6 +30,8 @@ int main(int argc, char** argv) {
     qt::small_sincos(a, &ss, &cs);
     qt::sincos_tilt(a, &st, &ct);
     qt::rate_sincos(a, &sr, &cr);
+    double sq, cq;
+    qt::resid_sincos(a, &sq, &cq);
     fwrite(&s, 8, 1, o);
     fwrite(&c, 8, 1, o);
     fwrite(&m, 8, 1, o);
@@ -39,6 +41,8 @@ int main(int argc, char** argv) {
     fwrite(&ct, 8, 1, o);
     fwrite(&sr, 8, 1, o);
     fwrite(&cr, 8, 1, o);
+    fwrite(&sq, 8, 1, o);
+    fwrite(&cq, 8, 1, o);
   }
   fclose(o);
   return 0;
@@ -58,7 +62,7 @@ def probe(tmp_path_factory):
         x = np.ascontiguousarray(x, dtype=np.float64)
         (d / "in.bin").write_bytes(x.tobytes())
         subprocess.run([str(exe), str(d / "in.bin"), str(d / "out.bin")], check=True)
-        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 9)
+        return np.frombuffer((d / "out.bin").read_bytes(), dtype=np.float64).reshape(-1, 11)
 
     return run
 
@@ -149,6 +153,27 @@ def test_rate_sincos_accuracy(probe):
     c = base[:, 6] * cr - base[:, 5] * sr
     assert np.max(np.abs(s - np.sin(a + d))) <= 4.5e-16
     assert np.max(np.abs(c - np.cos(a + d))) <= 4.5e-16
+
+
+def test_residual_sincos_accuracy(probe, col=9, lim=4e-3):
+    """resid_sincos (|d| <= kStage3Angle: the yaw-at-rest step's third stage
+    from its second), which returns sin d and cos d - 1, and the rotation
+    rotate_cm built on it."""
+    rng = np.random.default_rng(5 + col)
+    d = np.concatenate([rng.uniform(-lim, lim, 200000), [0.0, -0.0, 1e-12, lim, -lim]])
+    out = probe(d)
+    sd, cm = out[:, col], out[:, col + 1]
+    assert np.max(ulp_err(sd, np.sin(d))[np.abs(d) > 1e-300]) <= 1.0
+    cm_ref = -2.0 * np.sin(0.5 * d) ** 2  # cos d - 1 without cancellation
+    # cos d - 1 is truncated (d^6 / 6!): absolute error, what the rotation sees
+    assert np.max(np.abs(cm - cm_ref) - 2 * np.spacing(np.abs(cm_ref))) <= 6e-18
+    a = rng.uniform(-np.pi / 3, np.pi / 3, d.size)
+    base = probe(a)
+    s0, c0 = base[:, 5], base[:, 6]
+    s = np.fma(c0, sd, np.fma(s0, cm, s0)) if hasattr(np, "fma") else s0 + (s0 * cm + c0 * sd)
+    c = np.fma(-s0, sd, np.fma(c0, cm, c0)) if hasattr(np, "fma") else c0 + (c0 * cm - s0 * sd)
+    assert np.max(np.abs(s - np.sin(a + d))) <= 3.4e-16
+    assert np.max(np.abs(c - np.cos(a + d))) <= 3.4e-16
 
 
 CR_SRC = r"""
