@@ -709,8 +709,13 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
 // launch keeps every SIMD busy where one launch per group would run each
 // group's waves alone (65,536 episodes of five groups: ~205 waves per launch
 // on 1,024 SIMDs), and wave count stays ceil(n / 64).
+// Two waves per SIMD: mixed batches are large (config 5: 1,048,576 episodes,
+// 16 waves per SIMD on one GPU, 2 on each of 8), and a second resident wave
+// issues in the first one's stall and encoding slots.  The register budget
+// of 256 spills ~58 VGPRs to scratch, and still: 27.7 -> 25.0 ms for config 5
+// on one GPU (occupancy 1: 256 VGPRs + 48 AGPRs).
 template <int KC, bool FF, bool KS>
-__global__ __launch_bounds__(kBlock) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                                  BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
   const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
   if (slot < 0) return;
