@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 4
+#define QT_ABI_VERSION 5
 
 /* error codes */
 #define QT_OK 0
@@ -321,6 +321,19 @@ int qt_summary(int64_t n, const double* met, double mu_ratio, double mu_err, dou
    bitwise reproducible for a given (n, nparts).  work: DEVICE [nparts * 11]. */
 int qt_summary_parts(int64_t n, const double* met, double mu_ratio, double mu_err, double* out, double* work,
                      int32_t nparts, void* stream);
+
+/* ABI 5.  The EvaluationSummary sums in numpy's own order, so that means and
+   stds equal np.mean / np.std (utils/metrics.py:380-384) bit for bit.
+   numpy reduces a contiguous float64 vector in blocks of 8192 elements,
+   adding each block's pairwise sum to a running total in block order; this
+   writes the blocks' pairwise sums, out[rows][ceil(n / 8192)] (device); the
+   caller adds them in order starting from 0.0.
+   pass 0: rows = on_target_ratio, mean_err, mean_effort (np.mean);
+   pass 1: rows = (on_target_ratio - mu_ratio)^2, (mean_err - mu_err)^2 as np.std
+   forms them (subtract, then multiply; no fused multiply-add), with mu the
+   pass-0 means. */
+int qt_summary_numpy(int64_t n, const double* met, int32_t pass, double mu_ratio, double mu_err, double* out,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -372,6 +372,111 @@ __global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, co
   sum_block_reduce(p, out);
 }
 
+// ------------------------------------------- numpy-order sums (np.add.reduce)
+// compute_evaluation_summary's np.mean / np.std (utils/metrics.py:382-384)
+// reduce a contiguous float64 vector.  numpy (2.2, the reference's pinned
+// dependency) walks it in buffer-sized blocks of kNpBlock elements and adds
+// each block's pairwise sum to the running total in order; pairwise_sum
+// (numpy/_core/src/umath/loops_utils.h.src): < 8 elements summed in order
+// from 0.0; <= 128 elements as 8 strided accumulators, combined
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail in order; larger halves
+// split at n/2 rounded down to a multiple of 8.  np.std sums (x - mean)^2
+// formed as a subtraction and a product (no fused multiply-add).  One
+// wavefront per block: lane 0 lists the leaves (<= 128 elements each, in
+// order), the lanes sum them, lane 0 combines them along the same tree.  The
+// blocks' running total is the host's (a few per million episodes).
+constexpr int kNpBlock = 8192, kNpLeaf = 128, kNpMaxLeaves = 2 * kNpBlock / kNpLeaf;
+
+struct NpRows {
+  int row[3];
+  double mu[3];
+  int nrows, squares;
+};
+
+__device__ __forceinline__ int np_half(int m) { return m / 2 - (m / 2) % 8; }
+
+__device__ double np_leaf(const double* __restrict__ x, int lo, int len, bool sq, double mu) {
+#pragma clang fp contract(off)
+  auto val = [&](int i) {
+    const double v = x[lo + i];
+    if (!sq) return v;
+    const double d = v - mu;
+    return d * d;
+  };
+  if (len < 8) {
+    double r = 0.0;
+    for (int i = 0; i < len; ++i) r += val(i);
+    return r;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = val(j);
+  int i = 8;
+  for (; i < len - len % 8; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += val(i + j);
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < len; ++i) res += val(i);
+  return res;
+}
+
+// grid (blocks, rows): out[row][block] = pairwise sum of that block
+__global__ __launch_bounds__(64) void np_block_sum_kernel(int64_t n, const double* __restrict__ met, NpRows rs,
+                                                          double* __restrict__ out) {
+  __shared__ int leaf_lo[kNpMaxLeaves], leaf_len[kNpMaxLeaves];
+  __shared__ double leaf_sum[kNpMaxLeaves];
+  __shared__ int nleaves;
+  const int64_t lo = (int64_t)blockIdx.x * kNpBlock;
+  const int len = (int)(n - lo < kNpBlock ? n - lo : kNpBlock);
+  const double* x = met + (int64_t)rs.row[blockIdx.y] * n + lo;
+  if (threadIdx.x == 0) {  // leaves in order: depth-first, left half first
+    int st_lo[16], st_len[16], sp = 1, k = 0;
+    st_lo[0] = 0, st_len[0] = len;
+    while (sp > 0) {
+      --sp;
+      const int a = st_lo[sp], m = st_len[sp];
+      if (m <= kNpLeaf) {
+        leaf_lo[k] = a, leaf_len[k] = m, ++k;
+      } else {
+        const int m2 = np_half(m);
+        st_lo[sp] = a + m2, st_len[sp] = m - m2, ++sp;
+        st_lo[sp] = a, st_len[sp] = m2, ++sp;
+      }
+    }
+    nleaves = k;
+  }
+  __syncthreads();
+  const bool sq = rs.squares != 0;
+  const double mu = rs.mu[blockIdx.y];
+  for (int k = threadIdx.x; k < nleaves; k += 64) leaf_sum[k] = np_leaf(x, leaf_lo[k], leaf_len[k], sq, mu);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the same tree, each node = left + right
+    int fn[16], fs[16], sp = 1, k = 0;
+    double fv[16], ret = 0.0;
+    bool have = false;  // a child of the top frame returned `ret`
+    fn[0] = len, fs[0] = 0;
+    while (sp > 0) {
+      const int f = sp - 1;
+      if (have) {
+        if (fs[f] == 1) {  // left done: keep it, descend right
+          fv[f] = ret, fs[f] = 2, have = false;
+          fn[sp] = fn[f] - np_half(fn[f]), fs[sp] = 0, ++sp;
+        } else {
+          ret = fv[f] + ret, --sp;
+        }
+        continue;
+      }
+      if (fn[f] <= kNpLeaf) {
+        ret = leaf_sum[k++], have = true, --sp;
+        continue;
+      }
+      fs[f] = 1;
+      fn[sp] = np_half(fn[f]), fs[sp] = 0, ++sp;
+    }
+    out[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = ret;
+  }
+}
+
 // The exact step (also the deferred pass after a fast flavour: it takes the
 // waves the fast kernel left, see rollout_kernel).
 struct ExactLaunch {
@@ -592,6 +697,25 @@ int qt_summary_parts(int64_t n, const double* met, double mu_ratio, double mu_er
   hipStream_t s = (hipStream_t)stream;
   summary_part_kernel<<<nparts, kSumBlock, 0, s>>>(n, met, mu_ratio, mu_err, chunk, work);
   summary_final_kernel<<<1, kSumBlock, 0, s>>>(nparts, work, out);
+  return check_launch();
+}
+
+int qt_summary_numpy(int64_t n, const double* met, int32_t pass, double mu_ratio, double mu_err, double* out,
+                     void* stream) {
+  if (n < 0 || (pass != 0 && pass != 1) || (n > 0 && (!met || !out))) return QT_EINVAL;
+  if (n == 0) return QT_OK;
+  const int64_t nb = (n + kNpBlock - 1) / kNpBlock;
+  if (nb > (1ll << 30)) return QT_EINVAL;
+  NpRows rs{};
+  if (pass == 0) {
+    rs.row[0] = QT_MET_ON_TARGET_RATIO, rs.row[1] = QT_MET_MEAN_ERR, rs.row[2] = QT_MET_MEAN_EFFORT;
+    rs.nrows = 3, rs.squares = 0;
+  } else {
+    rs.row[0] = QT_MET_ON_TARGET_RATIO, rs.row[1] = QT_MET_MEAN_ERR;
+    rs.mu[0] = mu_ratio, rs.mu[1] = mu_err;
+    rs.nrows = 2, rs.squares = 1;
+  }
+  np_block_sum_kernel<<<dim3((unsigned)nb, rs.nrows), 64, 0, (hipStream_t)stream>>>(n, met, rs, out);
   return check_launch();
 }
 

@@ -339,6 +339,35 @@ def summary_partials(met: torch.Tensor, mu_ratio=0.0, mu_err=0.0, nparts: int | 
     return out
 
 
+NP_BLOCK = 8192  # numpy's reduction block (elements), qt_summary_numpy
+
+
+def summary_numpy_blocks(met: torch.Tensor, pass_: int, mu_ratio=0.0, mu_err=0.0) -> torch.Tensor:
+    """Per-block pairwise sums in numpy's order (qt_summary_numpy): pass 0 ->
+    [3, nblocks] (ratio, mean_err, mean_effort), pass 1 -> [2, nblocks] of the
+    squared deviations from (mu_ratio, mu_err).  Folding a row in block order
+    from 0.0 gives np.add.reduce of it bit for bit (np_fold)."""
+    lib = _abi.load()
+    n = met.shape[1]
+    if met.dim() != 2 or met.shape[0] != _abi.MET_ROWS or met.dtype != F64 or not met.is_contiguous():
+        raise ValueError("met must be a contiguous float64 [MET_ROWS, n] tensor")
+    nb = -(-n // NP_BLOCK)
+    out = torch.empty(3 if pass_ == 0 else 2, nb, dtype=F64, device=met.device)
+    if n:
+        with torch.cuda.device(met.device):
+            check(lib.qt_summary_numpy(n, ptr(met), int(pass_), float(mu_ratio), float(mu_err), ptr(out),
+                                       stream_of(met.device)), "qt_summary_numpy")
+    return out
+
+
+def np_fold(blocks) -> float:
+    """numpy's running total over block sums (in order, from 0.0)."""
+    s = 0.0
+    for v in blocks:
+        s += float(v)
+    return s
+
+
 def dare_batched(n_state: int, dt: float, gravity: float, mass: torch.Tensor | None, Q: torch.Tensor,
                  R: torch.Tensor, structured: bool):
     """Q [n_state*n_state, m], R [16, m] SoA -> (K [4*n_state, m], P [n_state^2, m], status int8 [m], iters int32 [m])."""

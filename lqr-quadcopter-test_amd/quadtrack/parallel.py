@@ -5,12 +5,15 @@ Episodes are independent, so a multi-GPU run is one process per GPU
 range of global episode indices; seeds and per-episode parameters are
 functions of the global index, so results do not depend on the world size.
 The only communication is at the end: the EvaluationSummary
-(utils/metrics.py:341-390) reductions — sums for the means, a second centred
-pass for the population std (np.std), and an all-gather of each rank's
-best/worst episode for the first-occurrence argmax/argmin.
+(utils/metrics.py:341-390) reductions — the means and population stds in
+numpy's own summation order (per-block pairwise sums, qt_summary_numpy,
+gathered and folded in global block order), counts, and an all-gather of
+each rank's best/worst episode for the first-occurrence argmax/argmin.
 """
 
 from __future__ import annotations
+
+import math
 
 import torch
 import torch.distributed as dist
@@ -74,15 +77,57 @@ def summary_from_stats(sums: list[float], m2: list[float], best: int, worst: int
     succ = int(round(sums[3]))
     return EvaluationSummary(
         total_episodes=count, successful_episodes=succ, success_rate=succ / count, mean_on_target_ratio=mu_r,
-        std_on_target_ratio=(m2[0] / count) ** 0.5, mean_tracking_error=mu_e,
-        std_tracking_error=(m2[1] / count) ** 0.5, mean_control_effort=sums[2] / count, best_episode_idx=best,
+        std_on_target_ratio=math.sqrt(m2[0] / count), mean_tracking_error=mu_e,
+        std_tracking_error=math.sqrt(m2[1] / count), mean_control_effort=sums[2] / count, best_episode_idx=best,
         worst_episode_idx=worst, meets_criteria=mu_r >= min_ratio)
 
 
-def summary_from_partials(met: torch.Tensor, criteria, group=None, distributed=True, global_offset: int = 0):
+def _gather_padded(t: torch.Tensor, group=None) -> list[torch.Tensor]:
+    """all_gather of [r, c_rank] tensors whose column counts differ by rank
+    (padded to the largest); returns each rank's tensor at its own width, on
+    t's device."""
+    c = torch.tensor([float(t.shape[1])], dtype=F64, device=t.device)
+    widths = [int(v[0]) for v in all_gather_rows(c, group)]
+    cmax = max(widths)
+    pad = torch.zeros(t.shape[0], cmax, dtype=F64, device=t.device)
+    pad[:, :t.shape[1]] = t
+    src = pad.cpu() if dist.get_backend(group) == "gloo" else pad
+    out = [torch.empty_like(src) for _ in widths]
+    dist.all_gather(out, src, group=group)
+    return [o[:, :w].to(t.device) for o, w in zip(out, widths)]
+
+
+def _np_sums(met: torch.Tensor, pass_: int, mu_r: float, mu_e: float, group, use_dist: bool) -> list[float]:
+    """np.add.reduce of this pass's rows over every rank's episodes, in global
+    episode order (the shards tile the global range at multiples of the numpy
+    block, checked by the caller): each rank's block sums, gathered in rank
+    order, folded from 0.0."""
+    from . import core
+
+    blocks = core.summary_numpy_blocks(met, pass_, mu_r, mu_e)
+    if use_dist:
+        blocks = torch.cat(_gather_padded(blocks, group), dim=1)
+    return [core.np_fold(row) for row in blocks.cpu().tolist()]
+
+
+def _shard_layout(n: int, global_offset: int, device, group) -> list[tuple[int, int]]:
+    """(global offset, episodes) of every rank, in rank order."""
+    rows = all_gather_rows(torch.tensor([float(global_offset), float(n)], dtype=F64, device=device), group)
+    return [(int(o), int(c)) for o, c in rows]
+
+
+def summary_from_partials(met: torch.Tensor, criteria, group=None, distributed=True, global_offset: int = 0,
+                          exact: bool = True):
     """EvaluationSummary of per-episode metric rows [MET_ROWS, n] on this rank
-    (and, when torch.distributed is initialised, on every other rank): two
-    passes of the qt_summary kernel and three tiny collectives."""
+    (and, when torch.distributed is initialised, on every other rank).
+
+    exact (default): means and stds in numpy's summation order
+    (qt_summary_numpy), equal to the reference's np.mean / np.std
+    (utils/metrics.py:380-384) bit for bit on the same per-episode metrics.
+    When the ranks' shards do not start at multiples of numpy's 8,192-element
+    block (in rank order), the metric rows are all-gathered first (one
+    [MET_ROWS, N] copy per rank).  exact=False: the fixed-order tree sums of
+    qt_summary_parts (~1e-15 relative from numpy's), three tiny collectives."""
     from . import core
     from .utils.metrics import EvaluationSummary, SuccessCriteria
 
@@ -96,10 +141,6 @@ def summary_from_partials(met: torch.Tensor, criteria, group=None, distributed=T
     count = int(round(s[4]))
     if count == 0:
         return EvaluationSummary()
-    p2 = core.summary_partials(met, s[0] / count, s[1] / count)
-    m2 = p2[5:7].clone()
-    if use_dist:
-        all_reduce_sum(m2, group)
     ext = p1[7:11].clone()
     if met.shape[1] == 0:
         ext = torch.tensor([float("-inf"), -1.0, float("inf"), -1.0], dtype=F64, device=met.device)
@@ -108,7 +149,27 @@ def summary_from_partials(met: torch.Tensor, criteria, group=None, distributed=T
         ext[3] += global_offset
     parts = all_gather_rows(ext, group) if use_dist else [ext.cpu().tolist()]
     best, worst = pick_extremes(parts)
-    return summary_from_stats(s, m2.cpu().tolist(), best, worst, crit.min_on_target_ratio)
+    if exact:
+        src, np_dist = met, use_dist
+        if use_dist:
+            layout = _shard_layout(met.shape[1], global_offset, met.device, group)
+            pos, tiled = 0, True
+            for o, c in layout:
+                tiled = tiled and o == pos and (c == 0 or pos % core.NP_BLOCK == 0)
+                pos += c
+            if not tiled:  # numpy's blocks straddle shards: reduce the whole array on every rank
+                ordered = sorted(zip(layout, _gather_padded(met, group)), key=lambda z: z[0][0])
+                src = torch.cat([m for _, m in ordered], dim=1).contiguous()
+                np_dist = False
+        s[0:3] = _np_sums(src, 0, 0.0, 0.0, group, np_dist)
+        m2 = _np_sums(src, 1, s[0] / count, s[1] / count, group, np_dist)
+    else:
+        p2 = core.summary_partials(met, s[0] / count, s[1] / count)
+        m2t = p2[5:7].clone()
+        if use_dist:
+            all_reduce_sum(m2t, group)
+        m2 = m2t.cpu().tolist()
+    return summary_from_stats(s, m2, best, worst, crit.min_on_target_ratio)
 
 
 def reduce_summary(met: torch.Tensor, criteria, group=None, global_offset: int = 0):

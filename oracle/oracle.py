@@ -389,3 +389,58 @@ def rollout(e, c, cr, motion, pat, mass, hover, K, kcols, k_per_episode, x0, max
         _dp(_f64(hover)) if hover is not None else None, _dp(_f64(K)), kcols,
         (9 if kcols == 3 else 4 * kcols) if k_per_episode else 0, _dp(_f64(x0)), int(max_steps), _dp(met), _dp(xf), _dp(integ))
     return met, xf, integ, used
+
+
+# --------------------------------------------- numpy's summation order
+# compute_evaluation_summary (utils/metrics.py:380-384) takes np.mean / np.std
+# of per-episode lists.  numpy (the reference's dependency; 2.2 here) reduces a
+# contiguous float64 vector in buffer blocks of NP_BLOCK elements, adding each
+# block's pairwise sum (numpy/_core/src/umath/loops_utils.h.src,
+# pairwise_sum) to a running total in order.  Pure-Python restatement, the
+# checker of qt_summary_numpy; pinned against numpy itself in tests/test_oracle.py.
+NP_BLOCK = 8192
+
+
+def np_pairwise(a, lo: int, n: int) -> float:
+    if n < 8:
+        r = 0.0
+        for i in range(n):
+            r += a[lo + i]
+        return r
+    if n <= 128:
+        r = [a[lo + j] for j in range(8)]
+        i = 8
+        while i < n - n % 8:
+            for j in range(8):
+                r[j] += a[lo + i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += a[lo + i]
+            i += 1
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return np_pairwise(a, lo, n2) + np_pairwise(a, lo + n2, n - n2)
+
+
+def np_blocks(a) -> list[float]:
+    """Per-block pairwise sums of a float sequence (qt_summary_numpy's output)."""
+    a = [float(v) for v in a]
+    return [np_pairwise(a, lo, min(NP_BLOCK, len(a) - lo)) for lo in range(0, len(a), NP_BLOCK)]
+
+
+def np_sum(a) -> float:
+    """np.add.reduce of a 1-D float64 sequence, restated."""
+    s = 0.0
+    for v in np_blocks(a):
+        s += v
+    return s
+
+
+def np_mean_std(a) -> tuple[float, float]:
+    """(np.mean(a), np.std(a)) restated: mean = sum / n; std = sqrt(sum((x - mean) * (x - mean)) / n)."""
+    a = [float(v) for v in a]
+    n = len(a)
+    mu = np_sum(a) / n
+    return mu, float(np.sqrt(np_sum([(x - mu) * (x - mu) for x in a]) / n))

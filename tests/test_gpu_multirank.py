@@ -61,10 +61,74 @@ def test_two_rank_summary_equals_single():
         assert p.exitcode == 0
     for k in ("total_episodes", "successful_episodes", "best_episode_idx", "worst_episode_idx", "meets_criteria"):
         assert got[k] == ref[k], k
+    # numpy-order sums (qt_summary_numpy): shards of 1,500 are not aligned to
+    # numpy's 8,192-element blocks, so the rows are gathered and reduced whole
     for k in ("mean_on_target_ratio", "std_on_target_ratio", "mean_tracking_error", "std_tracking_error",
               "mean_control_effort"):
-        assert got[k] == pytest.approx(ref[k], rel=1e-12, abs=1e-15), k
+        assert got[k] == ref[k], k
     assert np.isfinite(got["mean_tracking_error"])
+
+
+# synthetic per-episode metrics: shard layouts aligned to numpy's blocks
+# (block sums gathered) and not (rows gathered), 3 ranks
+LAYOUTS = {"aligned": [(0, 8192), (8192, 16384), (16384, 19384)], "unaligned": [(0, 6000), (6000, 13001), (13001, 19384)]}
+
+
+def _synthetic_met(n):
+    from quadtrack._abi import MET, MET_ROWS
+
+    rng = np.random.default_rng(3)
+    met = np.zeros((MET_ROWS, n))
+    met[MET["on_target_ratio"]] = rng.integers(0, 3001, n) / 3000.0
+    met[MET["mean_tracking_error"]] = rng.lognormal(size=n)
+    met[MET["mean_control_effort"]] = rng.uniform(5, 15, n)
+    met[MET["success"]] = rng.integers(0, 2, n)
+    return met
+
+
+def _summary_rank(rank, world, port, layout, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "lqr-quadcopter-test_amd"))
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadtrack.parallel import summary_from_partials
+        from quadtrack.utils.metrics import SuccessCriteria
+
+        lo, hi = LAYOUTS[layout][rank]
+        met = torch.as_tensor(_synthetic_met(LAYOUTS[layout][-1][1])[:, lo:hi].copy(), device="cuda")
+        s = summary_from_partials(met, SuccessCriteria(), global_offset=lo)
+        if rank == 0:
+            q.put(s.to_dict())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
+def test_sharded_summary_numpy_bitwise(layout):
+    from quadtrack._abi import MET
+
+    met = _synthetic_met(LAYOUTS[layout][-1][1])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_summary_rank, args=(r, 3, port, layout, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    r, e, u = (met[MET[k]] for k in ("on_target_ratio", "mean_tracking_error", "mean_control_effort"))
+    assert (got["mean_on_target_ratio"], got["std_on_target_ratio"]) == (np.mean(r), np.std(r))
+    assert (got["mean_tracking_error"], got["std_tracking_error"]) == (np.mean(e), np.std(e))
+    assert got["mean_control_effort"] == np.mean(u)
+    assert got["best_episode_idx"] == int(np.argmax(r)) and got["worst_episode_idx"] == int(np.argmin(r))
 
 
 def _rccl_rank(port, q):

@@ -786,6 +786,59 @@ def test_summary_partials_multiblock(qt, nparts):
     assert a[9] == ratio.min() and int(a[10]) == int(np.argmin(ratio))
 
 
+@pytest.mark.parametrize("n", [1, 5, 8, 9, 127, 128, 129, 143, 1000, 8191, 8192, 8193, 16384 + 77, 100003])
+def test_summary_numpy_order_bitwise(qt, n):
+    """qt_summary_numpy's per-block pairwise sums equal the oracle's
+    restatement of numpy's order, and the EvaluationSummary means / stds equal
+    np.mean / np.std (utils/metrics.py:380-384) bit for bit."""
+    import oracle as O
+    from quadtrack import core
+    from quadtrack._abi import MET, MET_ROWS
+    from quadtrack.parallel import summary_from_partials
+    from quadtrack.utils.metrics import SuccessCriteria
+
+    rng = np.random.default_rng(n)
+    met = np.zeros((MET_ROWS, n))
+    r = rng.integers(0, 3001, n) / 3000.0
+    e = rng.lognormal(size=n) * 10.0 ** rng.uniform(-3, 3, n)
+    u = rng.uniform(5, 15, n)
+    met[MET["on_target_ratio"]], met[MET["mean_tracking_error"]], met[MET["mean_control_effort"]] = r, e, u
+    met[MET["success"]] = rng.integers(0, 2, n)
+    t = torch.as_tensor(met, device="cuda")
+    b0 = core.summary_numpy_blocks(t, 0).cpu().numpy()
+    assert b0.shape == (3, -(-n // 8192))
+    for row, a in enumerate((r, e, u)):
+        assert b0[row].tolist() == O.np_blocks(a)
+        assert core.np_fold(b0[row]) == np.add.reduce(a)
+    mu_r, mu_e = np.mean(r), np.mean(e)
+    b1 = core.summary_numpy_blocks(t, 1, mu_r, mu_e).cpu().numpy()
+    assert core.np_fold(b1[0]) == np.add.reduce((r - mu_r) * (r - mu_r))
+    assert core.np_fold(b1[1]) == np.add.reduce((e - mu_e) * (e - mu_e))
+    s = summary_from_partials(t, SuccessCriteria(), distributed=False)
+    assert (s.mean_on_target_ratio, s.std_on_target_ratio) == (np.mean(r), np.std(r))
+    assert (s.mean_tracking_error, s.std_tracking_error) == (np.mean(e), np.std(e))
+    assert s.mean_control_effort == np.mean(u)
+    assert s.best_episode_idx == int(np.argmax(r)) and s.worst_episode_idx == int(np.argmin(r))
+
+
+def test_summary_fixture_bitwise(qt):
+    """compute_evaluation_summary over the reference Evaluator's per-episode
+    metrics (tests/golden/evaluator_lqi.npz) gives the reference's
+    EvaluationSummary exactly."""
+    import json
+
+    from quadtrack.utils import metrics as M
+
+    d = np.load(os.path.join(GOLDEN, "evaluator_lqi.npz"))
+    fj = json.loads(str(d["fields_json"]))
+    for name in ("stationary_lqi", "linear_lqi_limit"):
+        eps = [M.EpisodeMetrics(**{k: (bool(v) if k == "success" else (int(v) if k == "overshoot_count" else float(v)))
+                                   for k, v in zip(fj["metrics"], row)}) for row in d[f"{name}_metrics"]]
+        s = M.compute_evaluation_summary(eps)
+        for k, v in zip(fj["summary"], d[f"{name}_summary"]):
+            assert float(getattr(s, k)) == float(v), (name, k)
+
+
 def test_evaluate_batched_vs_evaluator(qt):
     """Batched evaluator == the drop-in sequential Evaluator for LQR (no
     integral, so the carry-over of SURVEY F8 is moot)."""

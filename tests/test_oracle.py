@@ -211,3 +211,34 @@ def test_seed_draws_match_reset():
             np.testing.assert_array_equal(pat[:, 0], R[f"{m}_param"][:, 0])
         elif m == "sinusoidal":
             np.testing.assert_array_equal(pat[:, :3], R[f"{m}_param"])
+
+
+def test_numpy_order_sums_restated():
+    """oracle.np_sum / np_mean_std (numpy's blocked pairwise order, the
+    checker of qt_summary_numpy) equal np.add.reduce / np.mean / np.std bit
+    for bit, across the leaf (< 8, <= 128), split and block (8,192) edges."""
+    rng = np.random.default_rng(11)
+    for n in list(range(1, 140)) + [255, 256, 257, 1000, 8191, 8192, 8193, 9000, 16384 + 77, 40000]:
+        a = rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 4, n)
+        assert O.np_sum(a) == np.add.reduce(a), n
+        mu, sd = O.np_mean_std(a)
+        assert mu == np.mean(a) and sd == np.std(a), n
+
+
+def test_numpy_order_summary_fixture():
+    """The reference's own EvaluationSummary (tests/golden/evaluator_lqi.npz,
+    compute_evaluation_summary over the Evaluator's episodes) from the
+    restated means / stds of its per-episode metrics, bitwise."""
+    d = np.load(os.path.join(GOLDEN, "evaluator_lqi.npz"))
+    fj = json.loads(str(d["fields_json"]))
+    fields, summ = fj["metrics"], fj["summary"]
+    for name in ("stationary_lqi", "linear_lqi_limit"):
+        m = d[f"{name}_metrics"]
+        s = dict(zip(summ, d[f"{name}_summary"]))
+        r, e, u = (m[:, fields.index(k)] for k in ("on_target_ratio", "mean_tracking_error", "mean_control_effort"))
+        mu_r, sd_r = O.np_mean_std(r)
+        mu_e, sd_e = O.np_mean_std(e)
+        got = [mu_r, sd_r, mu_e, sd_e, O.np_sum(u) / len(u)]
+        ref = [s[k] for k in ("mean_on_target_ratio", "std_on_target_ratio", "mean_tracking_error",
+                              "std_tracking_error", "mean_control_effort")]
+        assert got == ref, name
