@@ -200,8 +200,102 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(qt_criteria cr, int64_t
   for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
 }
 
+// numpy's summation order (np.add.reduce of a contiguous float64 vector; see
+// np_block_sum_kernel below for the rules) restated for ONE thread summing K
+// sequences at once over the same index range, values from val(i, v[K]).
+constexpr int kNpBlock = 8192, kNpLeaf = 128, kNpMaxLeaves = 2 * kNpBlock / kNpLeaf;
+
+__device__ __forceinline__ int np_half(int m) { return m / 2 - (m / 2) % 8; }
+
+template <int K, class F>
+__device__ void np_leaf_seq(const F& val, int lo, int len, double* res) {
+#pragma clang fp contract(off)
+  double v[K];
+  if (len < 8) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) res[k] = 0.0;
+    for (int i = 0; i < len; ++i) {
+      val(lo + i, v);
+#pragma unroll
+      for (int k = 0; k < K; ++k) res[k] += v[k];
+    }
+    return;
+  }
+  double r[8][K];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) val(lo + j, r[j]);
+  int i = 8;
+  for (; i < len - len % 8; i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      val(lo + i + j, v);
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[j][k] += v[k];
+    }
+#pragma unroll
+  for (int k = 0; k < K; ++k) res[k] = ((r[0][k] + r[1][k]) + (r[2][k] + r[3][k])) + ((r[4][k] + r[5][k]) + (r[6][k] + r[7][k]));
+  for (; i < len; ++i) {
+    val(lo + i, v);
+#pragma unroll
+    for (int k = 0; k < K; ++k) res[k] += v[k];
+  }
+}
+
+// pairwise sum of [lo0, lo0 + len), len <= kNpBlock: depth-first over the
+// halves, each node = left + right
+template <int K, class F>
+__device__ void np_pairwise_seq(const F& val, int lo0, int len, double* out) {
+  int fn[16], flo[16], fs[16], sp = 1;
+  double fv[16][K], ret[K];
+  bool have = false;  // a child of the top frame returned `ret`
+  fn[0] = len, flo[0] = lo0, fs[0] = 0;
+  while (sp > 0) {
+    const int f = sp - 1;
+    if (have) {
+      if (fs[f] == 1) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) fv[f][k] = ret[k];
+        fs[f] = 2, have = false;
+        const int h = np_half(fn[f]);
+        flo[sp] = flo[f] + h, fn[sp] = fn[f] - h, fs[sp] = 0, ++sp;
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) ret[k] = fv[f][k] + ret[k];
+        --sp;
+      }
+      continue;
+    }
+    if (fn[f] <= kNpLeaf) {
+      np_leaf_seq<K>(val, flo[f], fn[f], ret);
+      have = true, --sp;
+      continue;
+    }
+    fs[f] = 1;
+    flo[sp] = flo[f], fn[sp] = np_half(fn[f]), fs[sp] = 0, ++sp;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = ret[k];
+}
+
+// np.add.reduce of [0, len): blocks of kNpBlock, folded in order from 0.0
+template <int K, class F>
+__device__ void np_sum_seq(const F& val, int len, double* out) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = 0.0;
+  for (int lo = 0; lo < len; lo += kNpBlock) {
+    double b[K];
+    np_pairwise_seq<K>(val, lo, len - lo < kNpBlock ? len - lo : kNpBlock, b);
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] += b[k];
+  }
+}
+
 // compute_episode_metrics over recorded arrays (utils/metrics.py:144-338):
-// one lane per episode streams its rows.
+// one lane per episode streams its rows for the max, on-target count and
+// overshoot machine; the means and sums (np.mean / np.sum of the row norms,
+// metrics.py:198-202, 330-332) are formed in numpy's order (np_sum_seq), with
+// the norms as np.linalg.norm(axis=1) forms them (squares added in order, no
+// fused multiply-add), so they equal the reference's bit for bit.
 __global__ __launch_bounds__(kBlock) void metrics_arrays_kernel(qt_criteria cr, int64_t n, int32_t max_steps,
                                                                 const double* __restrict__ qpos,
                                                                 const double* __restrict__ tpos,
@@ -214,17 +308,27 @@ __global__ __launch_bounds__(kBlock) void metrics_arrays_kernel(qt_criteria cr, 
   Acc a{0, 0, -INFINITY, 0, 0, 0, 0, 0, 0, -1, -1, 0, 0, 0};
   const int S = steps[e] < max_steps ? steps[e] : max_steps;
   const double R = cr.target_radius;
-  for (int s = 0; s < S; ++s) {
+  // step s -> (err, err * err, |u|)
+  auto vals = [&](int s, double* v) {
+#pragma clang fp contract(off)
     const int64_t b3 = (int64_t)s * 3 * n + e, b4 = (int64_t)s * 4 * n + e;
     const double d0 = tpos[b3] - qpos[b3], d1 = tpos[b3 + n] - qpos[b3 + n], d2 = tpos[b3 + 2 * n] - qpos[b3 + 2 * n];
-    const double err = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-    a.sum_e += err;
-    a.sum_e2 += err * err;
+    const double err = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+    const double u0 = act[b4], u1 = act[b4 + n], u2 = act[b4 + 2 * n], u3 = act[b4 + 3 * n];
+    v[0] = err;
+    v[1] = err * err;
+    v[2] = sqrt(((u0 * u0 + u1 * u1) + u2 * u2) + u3 * u3);
+  };
+  double sums[3];
+  np_sum_seq<3>(vals, S, sums);
+  a.sum_e = sums[0], a.sum_e2 = sums[1], a.sum_u = sums[2];
+  for (int s = 0; s < S; ++s) {
+    double v[3];
+    vals(s, v);
+    const double err = v[0];
     if (!(err <= a.max_e) && !(a.max_e != a.max_e)) a.max_e = err;
     const bool on = err <= R;
     a.on_pre += on;
-    const double u0 = act[b4], u1 = act[b4 + n], u2 = act[b4 + 2 * n], u3 = act[b4 + 3 * n];
-    a.sum_u += sqrt(u0 * u0 + u1 * u1 + u2 * u2 + u3 * u3);
     if (a.prev_on >= 0) {
       overshoot_step(a, on, err - R, cr.overshoot_window);
     }
@@ -385,15 +489,11 @@ __global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, co
 // wavefront per block: lane 0 lists the leaves (<= 128 elements each, in
 // order), the lanes sum them, lane 0 combines them along the same tree.  The
 // blocks' running total is the host's (a few per million episodes).
-constexpr int kNpBlock = 8192, kNpLeaf = 128, kNpMaxLeaves = 2 * kNpBlock / kNpLeaf;
-
 struct NpRows {
   int row[3];
   double mu[3];
   int nrows, squares;
 };
-
-__device__ __forceinline__ int np_half(int m) { return m / 2 - (m / 2) % 8; }
 
 __device__ double np_leaf(const double* __restrict__ x, int lo, int len, bool sq, double mu) {
 #pragma clang fp contract(off)

@@ -175,9 +175,9 @@ class MappedBlock:
         self._off = (off + size + 63) & ~63
         return self._raw[off:off + size].view(dt).reshape(shape), C.c_void_p(self.dev + off)
 
-    def __del__(self):
+    def __del__(self, _vp=C.c_void_p):  # bound at definition: module globals may be gone at interpreter exit
         if getattr(self, "host", None):
-            self._lib.qt_host_free(C.c_void_p(self.host))
+            self._lib.qt_host_free(_vp(self.host))
             self.host = None
 
 
