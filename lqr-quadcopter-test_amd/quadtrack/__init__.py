@@ -22,7 +22,7 @@ from .controllers import (
     solve_dare,
 )
 from .env import BatchedQuadcopterEnv, EnvConfig, QuadcopterEnv, TargetMotion
-from .eval import BatchedEvaluator, Evaluator, evaluate_batched, load_controller
+from .eval import BatchedEvaluator, Evaluator, evaluate_batched, load_controller, run_hyperparameter_sweep
 from .rollout import RolloutResult, run_closed_loop
 from .utils import EpisodeMetrics, EvaluationSummary, SuccessCriteria, compute_episode_metrics
 
@@ -31,5 +31,5 @@ __version__ = "0.1.0"
 __all__ = ["BaseController", "BatchedLQR", "BatchedPID", "BatchedRiccatiLQR", "LQRController", "PIDController",
            "RiccatiLQRController", "batched_controller", "solve_dare",
            "BatchedQuadcopterEnv", "EnvConfig", "QuadcopterEnv", "TargetMotion", "Evaluator", "BatchedEvaluator", "evaluate_batched",
-           "load_controller", "RolloutResult", "run_closed_loop", "EpisodeMetrics", "EvaluationSummary",
+           "load_controller", "run_hyperparameter_sweep", "RolloutResult", "run_closed_loop", "EpisodeMetrics", "EvaluationSummary",
            "SuccessCriteria", "compute_episode_metrics", "_abi"]

@@ -243,3 +243,85 @@ class BatchedEvaluator:
         paths["metrics"].write_text(json.dumps(summary.to_dict(), indent=2))
         paths["report"].write_text(format_metrics_report(summary))
         return paths
+
+
+def _stateless(controller) -> bool:
+    """True when compute_action keeps no state from one episode to the next,
+    so a fresh controller per episode (batched) gives the sequential
+    Evaluator's episodes: LQR, and Riccati-LQR without its LQI integral (or on
+    its heuristic fallback, riccati_lqr.py:764-776, which ignores LQI)."""
+    if isinstance(controller, LQRController):
+        return True
+    if isinstance(controller, RiccatiLQRController):
+        return not controller.use_lqi or controller.fallback_controller is not None
+    return False
+
+
+def run_hyperparameter_sweep(sweep_config_path: str | Path, output_dir: str | Path = "reports/sweeps",
+                             batched: bool | str = "auto") -> list[dict]:
+    """Evaluation sweep over controller configurations (eval.py:516-628):
+    each entry of the YAML's `configurations` builds a controller
+    (`controller_type`, `controller_config`), an EnvConfig (`env_config`) and
+    SuccessCriteria (`criteria`), is evaluated over `num_episodes` seeded
+    episodes (`seed`), and the valid results are ranked by mean on-target
+    ratio and written to `output_dir/sweep_results.json`; a configuration that
+    raises is logged and left out of the ranking, as the reference does.
+
+    batched: "auto" (default) runs a configuration whose controller carries
+    no state between episodes (`_stateless`) as one fused launch
+    (evaluate_batched) and the others through the sequential Evaluator, whose
+    controller is never reset; True runs every configuration
+    batched (a fresh controller per episode); False runs all sequentially."""
+    import yaml
+
+    with open(sweep_config_path) as f:
+        sweep_config = yaml.safe_load(f)
+    output_dir = Path(output_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    results = []
+    configs = sweep_config.get("configurations", [])
+    logger.info("Running sweep with %d configurations", len(configs))
+    for i, config in enumerate(configs):
+        name = config.get("name", f"config_{i}")
+        logger.info("Configuration %d/%d: %s", i + 1, len(configs), config.get("name"))
+        try:
+            controller = load_controller(controller_type=config.get("controller_type", "deep"),
+                                         checkpoint_path=config.get("checkpoint_path"),
+                                         config=config.get("controller_config"))
+            env_config = EnvConfig.from_dict(config["env_config"]) if "env_config" in config else EnvConfig()
+            criteria = SuccessCriteria()
+            if "criteria" in config:
+                crit = config["criteria"]
+                criteria = SuccessCriteria(min_on_target_ratio=crit.get("min_on_target_ratio", 0.8),
+                                           min_episode_duration=crit.get("min_episode_duration", 30.0),
+                                           target_radius=crit.get("target_radius", 0.5))
+            num_episodes, seed = config.get("num_episodes", 5), config.get("seed", 42)
+            if batched is True or (batched == "auto" and _stateless(controller)):
+                (output_dir / name / "plots").mkdir(parents=True, exist_ok=True)  # as Evaluator() makes them
+                summary = evaluate_batched(controller, env_config, num_episodes=num_episodes, base_seed=seed,
+                                           criteria=criteria, with_episode_metrics=False)
+            else:
+                evaluator = Evaluator(controller=controller, env_config=env_config, criteria=criteria,
+                                      output_dir=output_dir / name)
+                summary = evaluator.evaluate(num_episodes=num_episodes, base_seed=seed, verbose=False)
+            results.append({"name": name, "config": config, "mean_on_target_ratio": summary.mean_on_target_ratio,
+                            "success_rate": summary.success_rate, "mean_tracking_error": summary.mean_tracking_error,
+                            "meets_criteria": summary.meets_criteria})
+            logger.info("  Result: on-target=%.1f%%, success=%.1f%%", summary.mean_on_target_ratio * 100,
+                        summary.success_rate * 100)
+        except Exception as e:  # eval.py:592-601
+            logger.error("Configuration %s failed: %s", config.get("name"), e)
+            results.append({"name": name, "config": config, "error": str(e)})
+    valid_results = [r for r in results if "error" not in r]
+    valid_results.sort(key=lambda x: x["mean_on_target_ratio"], reverse=True)
+    sweep_results_path = output_dir / "sweep_results.json"
+    with open(sweep_results_path, "w") as f:
+        json.dump(valid_results, f, indent=2)
+    logger.info("Saved sweep results: %s", sweep_results_path)
+    print("\n" + "=" * 60)
+    print("HYPERPARAMETER SWEEP RESULTS (Ranked)")
+    print("=" * 60)
+    for k, r in enumerate(valid_results):
+        print(f"{k + 1}. {r['name']}: on-target={r['mean_on_target_ratio']:.1%}, success={r['success_rate']:.1%}")
+    print("=" * 60)
+    return valid_results
