@@ -14,9 +14,11 @@ episodes in one fused rollout, then per-candidate scores.  Candidate
 generation follows the reference's random stream exactly
 (`_generate_random_config` 683-735: `default_rng(seed)`, parameters in its
 fixed order, one `uniform(lo, hi)` per component) and its grid order
-(`_generate_grid_configs` 737-830).  Search strategies that need sequential
-feedback (CMA-ES), result files and resume are the tuner's control plane and
-stay out of scope.
+(`_generate_grid_configs` 737-830).  Its data formats come along: TuningConfig
+/ TuningResult dictionaries, `resume_from` a previous results file, and the
+two files `tune()` writes (`_save_results`, 1103-1129).  CMA-ES needs the
+`cma` package's sequential ask / tell loop (absent here, as the reference
+itself then raises ImportError) and stays out of scope.
 
 Supported controller_type: "riccati_lqr" (per-candidate q_pos / q_vel /
 r_controls / q_int -> one DARE each), "pid" (kp_pos / ki_pos / kd_pos, the
@@ -30,9 +32,13 @@ ignored, as the reference's controllers ignore them.
 
 from __future__ import annotations
 
+import json
+import logging
+import os
 from dataclasses import dataclass, field, fields
 from datetime import datetime, timezone
 from itertools import product
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -43,6 +49,28 @@ from .controllers.riccati_lqr import BatchedRiccatiLQR
 from .env.config import EnvConfig
 from .rollout import run_closed_loop
 from .utils.metrics import SuccessCriteria
+
+logger = logging.getLogger(__name__)
+
+
+def _validate_path(path: Path) -> None:
+    """Path checks of tuning.py:64-106: no '..' or NUL, resolvable."""
+    path_str = str(path)
+    if ".." in path_str:
+        raise ValueError(f"Path contains path traversal sequence '..': {path}. "
+                         "Use absolute paths or paths without parent directory references.")
+    if "\x00" in path_str:
+        raise ValueError(f"Path contains null byte: {path}")
+    try:
+        resolved = path.resolve()
+        if not path.is_absolute():
+            try:
+                resolved.relative_to(Path.cwd().resolve())
+            except ValueError:
+                if len(resolved.parts) < 2:
+                    raise ValueError(f"Relative path resolves outside working directory: {path}")
+    except (OSError, RuntimeError) as e:
+        raise ValueError(f"Cannot resolve path {path}: {e}")
 
 # parameter name -> (range attribute, components); the order of
 # _generate_random_config (tuning.py:689-733)
@@ -128,7 +156,7 @@ def default_search_space(controller_type: str = "riccati_lqr") -> GainSearchSpac
 
 @dataclass
 class TuningConfig:
-    """Tuner settings (tuning.py:363-478); same defaults."""
+    """Tuner settings (tuning.py:363-478); same defaults and dictionary form."""
 
     controller_type: str = "pid"
     search_space: GainSearchSpace = field(default_factory=GainSearchSpace)
@@ -141,22 +169,41 @@ class TuningConfig:
     target_motion_type: str = "stationary"
     episode_length: float = 30.0
     target_radius: float = 0.5
+    output_dir: str = "reports/tuning"
+    resume_from: str | None = None
     feedforward_enabled: bool = False
+    cma_sigma0: float = 0.3
+    cma_popsize: int | None = None
 
     def __post_init__(self):
         if self.controller_type not in ("pid", "lqr", "riccati_lqr"):
-            raise ValueError(f"Invalid controller_type: '{self.controller_type}'")
+            raise ValueError(f"Invalid controller_type: '{self.controller_type}'. "
+                             "Valid choices are: pid, lqr, riccati_lqr")
         if self.strategy not in ("grid", "random", "cma_es"):
-            raise ValueError(f"Invalid strategy: '{self.strategy}'")
+            raise ValueError(f"Invalid strategy: '{self.strategy}'. Valid choices are: grid, random, cma_es")
         if self.max_iterations < 1:
             raise ValueError(f"max_iterations must be >= 1, got {self.max_iterations}")
         if self.evaluation_episodes < 1:
             raise ValueError(f"evaluation_episodes must be >= 1, got {self.evaluation_episodes}")
+        if self.cma_sigma0 <= 0:
+            raise ValueError(f"cma_sigma0 must be > 0, got {self.cma_sigma0}")
+        if self.cma_popsize is not None and self.cma_popsize < 2:
+            raise ValueError(f"cma_popsize must be >= 2, got {self.cma_popsize}")
+
+    @classmethod
+    def from_dict(cls, config: dict) -> "TuningConfig":
+        kw = {f.name: config.get(f.name, f.default) for f in fields(cls) if f.name != "search_space"}
+        return cls(search_space=GainSearchSpace.from_dict(config.get("search_space", {})), **kw)
+
+    def to_dict(self) -> dict:
+        d = {f.name: getattr(self, f.name) for f in fields(self)}
+        d["search_space"] = self.search_space.to_dict()
+        return d
 
 
 @dataclass
 class TuningResult:
-    """tuning.py:480-532 (no file I/O here)."""
+    """tuning.py:480-579: the result and its JSON file."""
 
     best_config: dict
     best_score: float
@@ -169,6 +216,29 @@ class TuningResult:
 
     def to_dict(self) -> dict:
         return {f.name: getattr(self, f.name) for f in fields(self)}
+
+    @classmethod
+    def from_dict(cls, data: dict) -> "TuningResult":
+        return cls(**{f.name: data[f.name] for f in fields(cls)})
+
+    def save(self, path: str | Path) -> Path:
+        path = Path(path)
+        _validate_path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(self.to_dict(), f, indent=2)
+        return path
+
+    @classmethod
+    def load(cls, path: str | Path) -> "TuningResult":
+        path = Path(path)
+        _validate_path(path)
+        if not path.exists():
+            raise FileNotFoundError(f"Tuning results file not found: {path}")
+        if not path.is_file():
+            raise ValueError(f"Path is not a file: {path}")
+        with open(path) as f:
+            return cls.from_dict(json.load(f))
 
 
 def random_configs(space: GainSearchSpace, n: int, rng: np.random.Generator) -> list[dict]:
@@ -257,6 +327,8 @@ class BatchedTuner:
         self.best_config: dict = {}
         self.best_score = float("-inf")
         self.best_metrics: dict = {}
+        self.output_dir = Path(os.environ.get("TUNING_OUTPUT_DIR", config.output_dir))  # tuning.py:627-628
+        _validate_path(self.output_dir)
 
     # ---- candidate generation (reference stream order)
     def generate_random_configs(self, n: int) -> list[dict]:
@@ -362,21 +434,44 @@ class BatchedTuner:
             self.best_score, self.best_config, self.best_metrics = score, cfg, metrics
 
     def tune(self) -> TuningResult:
-        """Random or grid search with all candidates evaluated in one batch."""
+        """Random or grid search (tuning.py:930-1001) with all candidates
+        evaluated in one batch: resume from `resume_from` (previous results and
+        best kept; a random search draws the remaining candidates from the
+        seed's stream, as the reference's fresh generator does), then the
+        results files of `_save_results`."""
         if self.config.strategy == "cma_es":
             raise NotImplementedError("CMA-ES is sequential; out of scope for the batched tuner")
+        if self.config.resume_from:
+            prev = TuningResult.load(self.config.resume_from)
+            self.results = prev.all_results
+            self.best_config, self.best_score, self.best_metrics = prev.best_config, prev.best_score, prev.best_metrics
         if self.config.strategy == "grid":
             configs = self.generate_grid_configs()[:self.config.max_iterations]
         else:
-            configs = self.generate_random_configs(self.config.max_iterations - len(self.results))
-        for cfg, (score, metrics) in zip(configs, self.evaluate_configs(configs)):
+            configs = self.generate_random_configs(max(0, self.config.max_iterations - len(self.results)))
+        for cfg, (score, metrics) in zip(configs, self.evaluate_configs(configs) if configs else []):
             self._record(cfg, score, metrics)
-        cfg_dict = {f.name: getattr(self.config, f.name) for f in fields(self.config)}
-        cfg_dict["search_space"] = self.config.search_space.to_dict()
-        return TuningResult(best_config=self.best_config, best_score=self.best_score,
-                            best_metrics=self.best_metrics, all_results=self.results,
-                            iterations_completed=len(self.results), interrupted=False,
-                            timestamp=datetime.now(timezone.utc).isoformat(), config=cfg_dict)
+        result = TuningResult(best_config=self.best_config, best_score=self.best_score,
+                              best_metrics=self.best_metrics, all_results=self.results,
+                              iterations_completed=len(self.results), interrupted=False,
+                              timestamp=datetime.now(timezone.utc).isoformat(), config=self.config.to_dict())
+        self.save_results(result)
+        return result
+
+    def save_results(self, result: TuningResult) -> dict[str, Path]:
+        """`<output_dir>/tuning_<type>_<UTC stamp>_results.json` (the full
+        result) and `..._best_config.json` (tuning.py:1103-1129)."""
+        self.output_dir.mkdir(parents=True, exist_ok=True)
+        stamp = datetime.now(timezone.utc).strftime("%Y%m%d_%H%M%S")
+        base = f"tuning_{self.config.controller_type}_{stamp}"
+        paths = {"results": result.save(self.output_dir / f"{base}_results.json"),
+                 "best_config": self.output_dir / f"{base}_best_config.json"}
+        with open(paths["best_config"], "w") as f:
+            json.dump({"controller_type": self.config.controller_type,
+                       self.config.controller_type: result.best_config,
+                       "metrics": result.best_metrics, "score": result.best_score}, f, indent=2)
+        logger.info("Saved tuning results to %s", self.output_dir)
+        return paths
 
 
 __all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "random_configs", "grid_configs",

@@ -1,0 +1,81 @@
+"""Tuner data formats (controllers/tuning.py:363-579, 930-1129) against the
+reference's own output (tests/golden/gen_tuning.py): TuningConfig /
+TuningResult dictionaries and files, the two files tune() writes, and
+resume_from a previous results file."""
+
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+
+FIX = json.load(open(os.path.join(GOLDEN, "tuning_results.json")))
+
+
+def _norm(d):
+    return json.loads(json.dumps(d))
+
+
+def test_tuning_config_dict_form():
+    from quadtrack.tuning import TuningConfig
+
+    cfg = TuningConfig.from_dict(FIX["base"])
+    d = _norm(cfg.to_dict())
+    d.pop("output_dir")
+    assert d == FIX["first"]["config"]
+    assert TuningConfig.from_dict(cfg.to_dict()).to_dict() == cfg.to_dict()
+    for bad in ({"controller_type": "deep"}, {"strategy": "bayes"}, {"max_iterations": 0}, {"cma_sigma0": 0.0},
+                {"cma_popsize": 1}, {"evaluation_episodes": 0}):
+        with pytest.raises(ValueError):
+            TuningConfig.from_dict(dict(FIX["base"], **bad))
+
+
+def test_tuning_result_file_round_trip(tmp_path):
+    from quadtrack.tuning import TuningResult
+
+    res = TuningResult.from_dict(dict(FIX["first_results_file"], timestamp="t"))
+    p = res.save(tmp_path / "r" / "x_results.json")
+    assert TuningResult.load(p).to_dict() == res.to_dict()
+    with pytest.raises(FileNotFoundError):
+        TuningResult.load(tmp_path / "missing.json")
+    with pytest.raises(ValueError):
+        TuningResult.load(tmp_path / ".." / "x.json")
+
+
+def _check_results(got, ref):
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        assert _norm(g["config"]) == r["config"]
+        assert g["score"] == pytest.approx(r["score"], rel=1e-8, abs=1e-10)
+        for k, v in r["metrics"].items():
+            assert g["metrics"][k] == pytest.approx(v, rel=1e-8, abs=1e-10), k
+
+
+@pytest.mark.gpu
+def test_tune_files_and_resume(tmp_path):
+    import glob
+
+    from quadtrack.tuning import BatchedTuner, TuningConfig, TuningResult
+
+    res = BatchedTuner(TuningConfig.from_dict(dict(FIX["base"], output_dir=str(tmp_path / "a")))).tune()
+    _check_results(res.all_results, FIX["first"]["all_results"])
+    assert _norm(res.best_config) == FIX["first"]["best_config"]
+    assert res.iterations_completed == 3 and res.interrupted is False
+    files = sorted(glob.glob(str(tmp_path / "a" / "tuning_riccati_lqr_*")))
+    assert len(files) == 2 and files[0].endswith("_best_config.json") and files[1].endswith("_results.json")
+    best = json.load(open([f for f in files if f.endswith("_best_config.json")][0]))
+    assert sorted(best) == sorted(FIX["first_best_config_file"])
+    assert _norm(best["riccati_lqr"]) == FIX["first_best_config_file"]["riccati_lqr"]
+    assert TuningResult.load([f for f in files if f.endswith("_results.json")][0]).to_dict() == _norm(res.to_dict())
+
+    # resume from the reference's own results file
+    prev = tmp_path / "prev_results.json"
+    prev.write_text(json.dumps(dict(FIX["first_results_file"], timestamp="t", config=dict(
+        FIX["first_results_file"]["config"], output_dir=str(tmp_path / "a")))))
+    res2 = BatchedTuner(TuningConfig.from_dict(dict(FIX["base"], max_iterations=5, resume_from=str(prev),
+                                                    output_dir=str(tmp_path / "b")))).tune()
+    assert res2.all_results[:3] == FIX["first_results_file"]["all_results"]  # carried over as loaded
+    _check_results(res2.all_results, FIX["resumed"]["all_results"])
+    assert res2.iterations_completed == FIX["resumed"]["iterations_completed"]
+    assert _norm(res2.best_config) == FIX["resumed"]["best_config"]
