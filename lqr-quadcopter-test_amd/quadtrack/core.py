@@ -348,9 +348,11 @@ def summary_numpy_blocks(met: torch.Tensor, pass_: int, mu_ratio=0.0, mu_err=0.0
     squared deviations from (mu_ratio, mu_err).  Folding a row in block order
     from 0.0 gives np.add.reduce of it bit for bit (np_fold)."""
     lib = _abi.load()
-    n = met.shape[1]
     if met.dim() != 2 or met.shape[0] != _abi.MET_ROWS or met.dtype != F64 or not met.is_contiguous():
         raise ValueError("met must be a contiguous float64 [MET_ROWS, n] tensor")
+    if pass_ not in (0, 1):
+        raise ValueError("pass_ must be 0 (sums) or 1 (squared deviations)")
+    n = met.shape[1]
     nb = -(-n // NP_BLOCK)
     out = torch.empty(3 if pass_ == 0 else 2, nb, dtype=F64, device=met.device)
     if n:
