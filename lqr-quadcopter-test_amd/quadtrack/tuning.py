@@ -319,6 +319,11 @@ class BatchedTuner:
 
     def __init__(self, config: TuningConfig, device=None, base_controller_config: dict | None = None):
         config.search_space.validate()
+        if config.strategy == "cma_es":  # tuning.py:636-643
+            try:
+                import cma  # noqa: F401
+            except ImportError:
+                raise ImportError("CMA-ES strategy requires the 'cma' package. Install it with: pip install cma")
         self.config = config
         self.device = device
         self.base = dict(base_controller_config or {})
@@ -427,6 +432,10 @@ class BatchedTuner:
                                        "success_rate": float(rate), "episodes_evaluated": E}))
         return out
 
+    def _evaluate_config(self, controller_config: dict) -> tuple[float, dict]:
+        """One candidate's (score, metrics), as tuning.py:846-928 returns them."""
+        return self.evaluate_configs([controller_config])[0]
+
     def _record(self, cfg, score, metrics):
         """tuning.py:1075-1088 (strictly-greater best update)."""
         self.results.append({"config": cfg, "score": score, "metrics": metrics})
@@ -474,5 +483,8 @@ class BatchedTuner:
         return paths
 
 
-__all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "random_configs", "grid_configs",
+# the reference's class name (controllers/tuning.py:581): same constructor and tune()
+ControllerTuner = BatchedTuner
+
+__all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "ControllerTuner", "random_configs", "grid_configs",
            "default_search_space"]

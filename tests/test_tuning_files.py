@@ -79,3 +79,27 @@ def test_tune_files_and_resume(tmp_path):
     _check_results(res2.all_results, FIX["resumed"]["all_results"])
     assert res2.iterations_completed == FIX["resumed"]["iterations_completed"]
     assert _norm(res2.best_config) == FIX["resumed"]["best_config"]
+
+
+def test_cma_es_without_cma_raises_import_error():
+    """As the reference's ControllerTuner does when `cma` is absent (tuning.py:636-643)."""
+    import importlib.util
+
+    from quadtrack.tuning import ControllerTuner, TuningConfig
+
+    if importlib.util.find_spec("cma") is not None:
+        pytest.skip("cma installed")
+    with pytest.raises(ImportError, match="cma"):
+        ControllerTuner(TuningConfig.from_dict(dict(FIX["base"], strategy="cma_es")))
+
+
+@pytest.mark.gpu
+def test_controller_tuner_evaluate_config(tmp_path):
+    """The reference's name and single-candidate entry point."""
+    from quadtrack.tuning import ControllerTuner, TuningConfig
+
+    t = ControllerTuner(TuningConfig.from_dict(dict(FIX["base"], output_dir=str(tmp_path))))
+    for r in FIX["first"]["all_results"]:
+        score, metrics = t._evaluate_config(r["config"])
+        assert score == pytest.approx(r["score"], rel=1e-8, abs=1e-10)
+        assert metrics["mean_on_target_ratio"] == pytest.approx(r["metrics"]["mean_on_target_ratio"], rel=1e-8)
