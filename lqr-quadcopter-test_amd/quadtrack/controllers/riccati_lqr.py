@@ -443,8 +443,6 @@ class BatchedRiccatiLQR:
         self.n_state = 9 if self.use_lqi else 6
         self.k_cols = self.n_state
         base_mass = float(config.get("mass", 1.0))
-        if isinstance(mass, torch.Tensor):
-            mass = mass.detach().to("cpu", torch.float64).numpy()
         per_arrays = (q_pos, q_vel, r_controls, q_int, mass, Q, R, ff_velocity_gain, ff_acceleration_gain)
         per = [a is not None for a in per_arrays]
         lens = [len(a) for a in per_arrays if a is not None]
@@ -454,6 +452,7 @@ class BatchedRiccatiLQR:
         self.per_episode = any(per)
         self.num_problems = m
         qi = _validate_q_int(config.get("q_int", [0.0, 0.0, 0.0]))
+        n = self.n_state
         # shared full Q / R from the config (RiccatiLQRController's "Q" / "R" keys,
         # riccati_lqr.py:568-577, 637-641), unless per-episode arrays are given
         if Q is None and config.get("Q") is not None:
@@ -462,15 +461,18 @@ class BatchedRiccatiLQR:
         if R is None and config.get("R") is not None:
             R = np.broadcast_to(_build_R(config).astype(float), (m, 4, 4)).copy()
         if Q is None:
-            Qd = np.empty((m, self.n_state))
+            # diagonal weights (every BASELINE config and the tuner's candidates):
+            # the diagonals go to the device as [n, m] and the SoA matrices are
+            # filled there, no [m, n, n] host arrays
+            Qd = np.empty((m, n))
             Qd[:, 0:3] = np.broadcast_to(np.asarray(q_pos if q_pos is not None else config.get("q_pos", [1e-4, 1e-4, 16.0]), float), (m, 3))
             Qd[:, 3:6] = np.broadcast_to(np.asarray(q_vel if q_vel is not None else config.get("q_vel", [0.0036, 0.0036, 4.0]), float), (m, 3))
             if self.use_lqi:
                 qq = np.asarray(q_int, float) if q_int is not None else qi
                 Qd[:, 6:9] = np.broadcast_to(qq, (m, 3))
-            Qm = np.zeros((m, self.n_state, self.n_state))
-            idx = np.arange(self.n_state)
-            Qm[:, idx, idx] = Qd
+            Q_soa = torch.zeros(n * n, m, dtype=torch.float64, device=dev)
+            Q_soa[torch.arange(n, device=dev) * (n + 1)] = torch.as_tensor(np.array(Qd.T, order="C"), device=dev)
+            q_diag = not bool(np.isnan(Qd).any())  # as Q == Q * I judges a NaN weight: the dense solver
         else:
             Qm = np.asarray(Q, float)
             if self.use_lqi and Qm.shape[1:] == (6, 6):
@@ -478,20 +480,30 @@ class BatchedRiccatiLQR:
                 Qa[:, :6, :6] = Qm
                 Qa[:, 6:, 6:] = np.diag(qi)
                 Qm = Qa
+            if Qm.shape != (m, n, n):
+                raise ValueError(f"per-episode Q / R must be [{m},{n},{n}] / [{m},4,4]")
+            q_diag = bool(np.all(Qm == Qm * np.eye(n)))
+            Q_soa = _soa(Qm, dev)
         if R is None:
             rr = np.broadcast_to(np.asarray(r_controls if r_controls is not None else config.get("r_controls", [1.0] * 4), float), (m, 4))
-            Rm = np.zeros((m, 4, 4))
-            Rm[:, np.arange(4), np.arange(4)] = rr
+            R_soa = torch.zeros(16, m, dtype=torch.float64, device=dev)
+            R_soa[torch.arange(4, device=dev) * 5] = torch.as_tensor(np.array(rr.T, order="C"), device=dev)
+            r_diag = not bool(np.isnan(rr).any())
         else:
             Rm = np.asarray(R, float)
-        if Qm.shape != (m, self.n_state, self.n_state) or Rm.shape != (m, 4, 4):
-            raise ValueError(f"per-episode Q / R must be [{m},{self.n_state},{self.n_state}] / [{m},4,4]")
-        masses = np.broadcast_to(np.asarray(mass if mass is not None else base_mass, float), (m,)).copy()
-        structured = bool(np.all(Qm == Qm * np.eye(self.n_state)) and np.all(Rm == Rm * np.eye(4)))
+            if Rm.shape != (m, 4, 4):
+                raise ValueError(f"per-episode Q / R must be [{m},{n},{n}] / [{m},4,4]")
+            r_diag = bool(np.all(Rm == Rm * np.eye(4)))
+            R_soa = _soa(Rm, dev)
+        structured = q_diag and r_diag
         self.structured = structured
-        self.mass = torch.as_tensor(masses, device=dev)
+        if isinstance(mass, torch.Tensor):  # per-episode masses already on the device stay there
+            self.mass = mass.detach().to(device=dev, dtype=torch.float64).reshape(m).contiguous()
+        else:
+            self.mass = torch.as_tensor(
+                np.broadcast_to(np.asarray(mass if mass is not None else base_mass, float), (m,)).copy(), device=dev)
         self.K, self.P, self.status, self.iters = core.dare_batched(
-            self.n_state, self.dt, self.gravity, self.mass, _soa(Qm, dev), _soa(Rm, dev), structured)
+            self.n_state, self.dt, self.gravity, self.mass, Q_soa, R_soa, structured)
         self.k_structured = core.gains_structured(self.K, self.k_cols)
         self.fallback_on_failure = config.get("fallback_on_failure", True)
         bad = self.status != DARE_OK

@@ -60,6 +60,19 @@ def main():
                         plant_mass=sh.plant_mass, group_motion=not args.no_group)
     torch.cuda.synchronize()
     t_batch = time.perf_counter() - t0
+    # the same setup again, warm (kernels loaded, allocator primed): what a
+    # tuner pays per sweep after the first
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sh2 = workloads.build(args.config, lo, hi, device=dev)
+    torch.cuda.synchronize()
+    t_ctl_warm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    build_batch(sh2.controller, sh2.env_config, sh2.n, seeds=sh2.seeds, motion=sh2.motion,
+                plant_mass=sh2.plant_mass, group_motion=not args.no_group)
+    torch.cuda.synchronize()
+    t_batch_warm = time.perf_counter() - t0
+    del sh2
 
     env = sh.env_config.to_params()
     crit = _criteria(None)
@@ -98,6 +111,7 @@ def main():
             "config": args.config, "episodes": total, "world": world, "episodes_per_rank": sh.n,
             "grouped": batch.groups is not None,
             "setup_s": {"controller_dare_and_params": round(t_ctl, 4), "batch_draws": round(t_batch, 4)},
+            "setup_warm_s": {"controller_dare_and_params": round(t_ctl_warm, 4), "batch_draws": round(t_batch_warm, 4)},
             "dare_max_iterations": int(sh.controller.iters.max().item()),
             "dare_fallbacks": int((sh.controller.status != 0).sum().item()),
             "rollout_ms": round(kern, 3), "rollout_ms_median": round(sorted(times)[len(times) // 2], 3),
