@@ -69,6 +69,15 @@ def build_augmented_lqi_system(A: np.ndarray, B: np.ndarray, dt: float) -> tuple
     return A_aug, B_aug
 
 
+def _diag_rows(v, k: int, m: int, device) -> torch.Tensor:
+    """Diagonal weights -> [k, m] float64 on device: a shared k-vector is
+    broadcast on the device, per-episode [m, k] values are copied once."""
+    a = np.asarray(v, dtype=np.float64)
+    if a.size == k:
+        return torch.as_tensor(a.reshape(k, 1).copy(), device=device).expand(k, m)
+    return torch.as_tensor(np.array(np.broadcast_to(a, (m, k)).T, order="C"), device=device)
+
+
 def _soa(mats: np.ndarray, device) -> torch.Tensor:
     """[m, r, c] -> [r*c, m] float64 on device."""
     mats = np.asarray(mats, dtype=np.float64)
@@ -464,15 +473,16 @@ class BatchedRiccatiLQR:
             # diagonal weights (every BASELINE config and the tuner's candidates):
             # the diagonals go to the device as [n, m] and the SoA matrices are
             # filled there, no [m, n, n] host arrays
-            Qd = np.empty((m, n))
-            Qd[:, 0:3] = np.broadcast_to(np.asarray(q_pos if q_pos is not None else config.get("q_pos", [1e-4, 1e-4, 16.0]), float), (m, 3))
-            Qd[:, 3:6] = np.broadcast_to(np.asarray(q_vel if q_vel is not None else config.get("q_vel", [0.0036, 0.0036, 4.0]), float), (m, 3))
+            blocks = [(q_pos, config.get("q_pos", [1e-4, 1e-4, 16.0])),
+                      (q_vel, config.get("q_vel", [0.0036, 0.0036, 4.0]))]
             if self.use_lqi:
-                qq = np.asarray(q_int, float) if q_int is not None else qi
-                Qd[:, 6:9] = np.broadcast_to(qq, (m, 3))
+                blocks.append((q_int, qi))
             Q_soa = torch.zeros(n * n, m, dtype=torch.float64, device=dev)
-            Q_soa[torch.arange(n, device=dev) * (n + 1)] = torch.as_tensor(np.array(Qd.T, order="C"), device=dev)
-            q_diag = not bool(np.isnan(Qd).any())  # as Q == Q * I judges a NaN weight: the dense solver
+            q_diag = True
+            for b, (per_ep, shared_v) in enumerate(blocks):
+                d = _diag_rows(per_ep if per_ep is not None else shared_v, 3, m, dev)
+                q_diag = q_diag and not bool(torch.isnan(d).any())  # as Q == Q * I judges a NaN: the dense solver
+                Q_soa[torch.arange(3 * b, 3 * b + 3, device=dev) * (n + 1)] = d
         else:
             Qm = np.asarray(Q, float)
             if self.use_lqi and Qm.shape[1:] == (6, 6):
@@ -485,10 +495,10 @@ class BatchedRiccatiLQR:
             q_diag = bool(np.all(Qm == Qm * np.eye(n)))
             Q_soa = _soa(Qm, dev)
         if R is None:
-            rr = np.broadcast_to(np.asarray(r_controls if r_controls is not None else config.get("r_controls", [1.0] * 4), float), (m, 4))
+            d = _diag_rows(r_controls if r_controls is not None else config.get("r_controls", [1.0] * 4), 4, m, dev)
             R_soa = torch.zeros(16, m, dtype=torch.float64, device=dev)
-            R_soa[torch.arange(4, device=dev) * 5] = torch.as_tensor(np.array(rr.T, order="C"), device=dev)
-            r_diag = not bool(np.isnan(rr).any())
+            R_soa[torch.arange(4, device=dev) * 5] = d
+            r_diag = not bool(torch.isnan(d).any())
         else:
             Rm = np.asarray(R, float)
             if Rm.shape != (m, 4, 4):

@@ -283,8 +283,9 @@ def motion_groups(motion: np.ndarray):
     """Host grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end)."""
     motion = np.asarray(motion).reshape(-1)
     order = np.argsort(motion, kind="stable").astype(np.int32)
-    kinds, counts = np.unique(motion, return_counts=True)
-    return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts)]
+    counts = np.bincount(motion.astype(np.intp), minlength=5)  # motion types 0..4: O(n), no sort
+    kinds = np.nonzero(counts)[0]
+    return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts[kinds])]
 
 
 def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:

@@ -235,7 +235,7 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
     kinds = None if motion is None else motion_indices(motion, n)
     mo = None if kinds is None else torch.as_tensor(kinds, device=dev)
     groups = None
-    if kinds is not None and order is None and group_motion and len(np.unique(kinds)) > 1:
+    if kinds is not None and order is None and group_motion and kinds.size and np.any(kinds != kinds.flat[0]):
         order, seg_motion, seg_end = core.motion_groups(kinds)
         groups = (seg_motion, seg_end)
     if plant_mass is None:
