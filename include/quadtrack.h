@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 5
+#define QT_ABI_VERSION 6
 
 /* error codes */
 #define QT_OK 0
@@ -216,6 +216,15 @@ int qt_seed_draws(int64_t n, const int64_t* seeds, const int8_t* motion, int32_t
    DEVICE arrays; out[k][n]; k <= 64. */
 int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo, const double* hi,
                     double* out, void* stream);
+
+/* ABI 6.  Draw vectors first .. first+n-1 of ONE stream
+   numpy.random.default_rng(seed).uniform(lo, hi, size=(first + n, k)): lane i
+   jumps the PCG64 state k * (first + i) outputs ahead (PCG64.advance) and draws
+   its k uniforms, so a shard of a long candidate stream needs none of the draws
+   before it (controllers/tuning.py:683-735's random candidates, SURVEY §8d
+   config 4).  lo, hi: [k] DEVICE arrays; out[k][n]; k <= 64. */
+int qt_stream_uniform(uint64_t seed, int64_t first, int64_t n, int32_t k, const double* lo, const double* hi,
+                      double* out, void* stream);
 
 /* The fused closed loop: `nsteps` iterations of
    compute_action (riccati_lqr.py:779-967; k_cols 3: PIDController.compute_action,

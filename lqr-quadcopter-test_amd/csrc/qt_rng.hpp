@@ -102,6 +102,23 @@ QT_RNG_HD Pcg64 pcg64_from_seed(uint64_t seed) {
   return g;
 }
 
+// Jump the generator `delta` outputs ahead (numpy's PCG64.advance:
+// pcg_setseq_128_advance_r, the LCG's jump-ahead by squaring, O(log delta)).
+QT_RNG_HD void pcg_advance(Pcg64& g, u128 delta) {
+  u128 cur_mult = ((u128)kPcgMultHi << 64) | kPcgMultLo, cur_plus = g.inc;
+  u128 acc_mult = 1, acc_plus = 0;
+  while (delta > 0) {
+    if (delta & 1) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    delta >>= 1;
+  }
+  g.state = acc_mult * g.state + acc_plus;
+}
+
 QT_RNG_HD uint64_t pcg_next64(Pcg64& g) {
   pcg_step(g);
   const uint64_t x = (uint64_t)(g.state >> 64) ^ (uint64_t)g.state;

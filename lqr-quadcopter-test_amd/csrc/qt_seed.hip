@@ -57,7 +57,30 @@ __global__ __launch_bounds__(256) void seed_uniform_kernel(int64_t n, const int6
   for (int j = 0; j < k; ++j) out[(int64_t)j * n + e] = lo[j] + (hi[j] - lo[j]) * qt::pcg_next_double(g);
 }
 
+// Draw vectors first .. first+n-1 of ONE stream default_rng(seed): lane i
+// jumps the generator k * (first + i) outputs ahead and draws its k uniforms,
+// lo + (hi - lo) * next_double as numpy's uniform forms them.
+__global__ __launch_bounds__(256) void stream_uniform_kernel(uint64_t seed, int64_t first, int64_t n, int32_t k,
+                                                             const double* __restrict__ lo,
+                                                             const double* __restrict__ hi, double* out) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  qt::Pcg64 g = qt::pcg64_from_seed(seed);
+  qt::pcg_advance(g, (qt::u128)(uint64_t)(first + i) * (uint64_t)k);
+  for (int j = 0; j < k; ++j) out[(int64_t)j * n + i] = lo[j] + (hi[j] - lo[j]) * qt::pcg_next_double(g);
+}
+
 }  // namespace
+
+extern "C" int qt_stream_uniform(uint64_t seed, int64_t first, int64_t n, int32_t k, const double* lo,
+                                 const double* hi, double* out, void* stream) {
+  if (n < 0 || first < 0 || k < 0 || k > 64) return QT_EINVAL;
+  if (n == 0 || k == 0) return QT_OK;  // empty: no pointer is read
+  if (!lo || !hi || !out) return QT_EINVAL;
+  stream_uniform_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(seed, first, n, k, lo, hi, out);
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
+}
 
 extern "C" int qt_seed_uniform(int64_t n, const int64_t* seeds, int32_t k, const double* lo, const double* hi,
                                double* out, void* stream) {

@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
 LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # enums (include/quadtrack.h)
 MOTIONS = ("stationary", "linear", "circular", "sinusoidal", "figure8")
@@ -82,7 +82,7 @@ class State(C.Structure):
 EXPORTS = ("qt_abi_version", "qt_host_alloc", "qt_host_free", "qt_stream_sync", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_grouped",
            "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary",
-           "qt_summary_parts", "qt_summary_numpy")
+           "qt_summary_parts", "qt_summary_numpy", "qt_stream_uniform")
 
 _lib = None
 
@@ -121,6 +121,7 @@ def load():
     L.qt_summary.argtypes = [i64, vp, dbl, dbl, vp, vp]
     L.qt_summary_parts.argtypes = [i64, vp, dbl, dbl, vp, vp, i32, vp]
     L.qt_summary_numpy.argtypes = [i64, vp, i32, dbl, dbl, vp, vp]
+    L.qt_stream_uniform.argtypes = [C.c_uint64, i64, i64, i32, vp, vp, vp, vp]
     for name in EXPORTS[1:]:
         getattr(L, name).restype = C.c_int
     v = L.qt_abi_version()

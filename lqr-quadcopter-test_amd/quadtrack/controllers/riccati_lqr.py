@@ -72,6 +72,9 @@ def build_augmented_lqi_system(A: np.ndarray, B: np.ndarray, dt: float) -> tuple
 def _diag_rows(v, k: int, m: int, device) -> torch.Tensor:
     """Diagonal weights -> [k, m] float64 on device: a shared k-vector is
     broadcast on the device, per-episode [m, k] values are copied once."""
+    if isinstance(v, torch.Tensor):  # device draws (workloads.tuner_candidate_tensors) stay on the device
+        t = v.detach().to(device=device, dtype=torch.float64)
+        return t.reshape(k, 1).expand(k, m) if t.numel() == k else t.reshape(m, k).T
     a = np.asarray(v, dtype=np.float64)
     if a.size == k:
         return torch.as_tensor(a.reshape(k, 1).copy(), device=device).expand(k, m)

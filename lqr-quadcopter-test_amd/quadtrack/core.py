@@ -307,6 +307,23 @@ def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:
     return out
 
 
+def stream_uniform(seed: int, first: int, n: int, lo, hi, device) -> torch.Tensor:
+    """Draw vectors first .. first+n-1 of default_rng(seed).uniform(lo, hi,
+    size=(., k)) -> [k, n] on the device (qt_stream_uniform)."""
+    lib = _abi.load()
+    if seed < 0 or first < 0 or n < 0:
+        raise ValueError("seed, first and n must be non-negative")
+    lo_t = to_device(np.atleast_1d(np.asarray(lo, float)), device)
+    hi_t = to_device(np.atleast_1d(np.asarray(hi, float)), device)
+    if lo_t.numel() != hi_t.numel() or lo_t.numel() > 64:
+        raise ValueError("lo and hi must have the same length k <= 64")
+    out = torch.empty(lo_t.numel(), n, dtype=F64, device=device)
+    with torch.cuda.device(device):
+        check(lib.qt_stream_uniform(int(seed), int(first), int(n), lo_t.numel(), ptr(lo_t), ptr(hi_t), ptr(out),
+                                    stream_of(device)), "qt_stream_uniform")
+    return out
+
+
 def episode_metrics(crit: Criteria, st: RolloutState) -> torch.Tensor:
     lib = _abi.load()
     n = st.t.numel()

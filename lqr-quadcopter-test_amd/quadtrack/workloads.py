@@ -89,6 +89,17 @@ def tuner_candidate_arrays(lo: int, hi: int, seed: int = TUNER_SEED) -> tuple[np
     return u[:, 0:3].copy(), u[:, 3:6].copy(), u[:, 6:10].copy()
 
 
+def tuner_candidate_tensors(lo: int, hi: int, device, seed: int = TUNER_SEED):
+    """tuner_candidate_arrays drawn on the device (qt_stream_uniform: each
+    candidate's lane jumps the one stream to its own draws), as [n, 3], [n, 3],
+    [n, 4] views of one [10, n] array; bitwise the same values."""
+    space = default_search_space("riccati_lqr")
+    lo_v = list(space.q_pos_range[0]) + list(space.q_vel_range[0]) + list(space.r_controls_range[0])
+    hi_v = list(space.q_pos_range[1]) + list(space.q_vel_range[1]) + list(space.r_controls_range[1])
+    u = core.stream_uniform(seed, lo, hi - lo, lo_v, hi_v, device)
+    return u[0:3].T, u[3:6].T, u[6:10].T
+
+
 def episode_masses(lo: int, hi: int, device) -> torch.Tensor:
     """default_rng(10**9 + i).uniform(0.8, 1.2) for i in [lo, hi), drawn on the
     device (qt_seed_uniform)."""
@@ -116,8 +127,9 @@ def build(config: int, lo: int | None = None, hi: int | None = None, device=None
     elif config == 3:
         ctl = BatchedRiccatiLQR(dict(LQI_CONFIG, dt=0.01), device=device)
     elif config == 4:
-        qp, qv, rc = tuner_candidate_arrays(lo, hi)
-        ctl = BatchedRiccatiLQR({"dt": 0.01}, device=device, q_pos=qp, q_vel=qv, r_controls=rc)
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        qp, qv, rc = tuner_candidate_tensors(lo, hi, dev)
+        ctl = BatchedRiccatiLQR({"dt": 0.01}, device=dev, q_pos=qp, q_vel=qv, r_controls=rc)
     else:
         motion = motion_of(lo, hi)
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -127,5 +139,6 @@ def build(config: int, lo: int | None = None, hi: int | None = None, device=None
 
 
 __all__ = ["EPISODES", "MOTION", "LQI_CONFIG", "Shard", "shard_bounds", "tuner_candidates", "tuner_candidate_arrays",
+           "tuner_candidate_tensors",
            "episode_masses",
            "motion_of", "build"]

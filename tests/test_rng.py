@@ -147,3 +147,50 @@ def test_device_reset_draws_mixed_motion():
         rp, ro = O.draws(m, idx + 10**9)
         np.testing.assert_array_equal(pat.cpu().numpy().T[idx], rp)
         np.testing.assert_array_equal(off.cpu().numpy().T[idx], ro)
+
+
+ADV_SRC = r"""
+#include <cstdio>
+#include <cstdlib>
+#include "qt_rng.hpp"
+int main(int argc, char** argv) {
+  const unsigned long long seed = strtoull(argv[1], 0, 10), d = strtoull(argv[2], 0, 10);
+  qt::Pcg64 g = qt::pcg64_from_seed(seed);
+  qt::pcg_advance(g, (qt::u128)d);
+  for (int i = 0; i < 4; ++i) printf("%llu\n", (unsigned long long)qt::pcg_next64(g));
+  return 0;
+}
+"""
+
+
+@pytest.mark.parametrize("seed,delta", [(42, 0), (42, 1), (7, 10 * 131071), (12345, 2**40 + 3), (2**63 - 1, 2**62)])
+def test_pcg64_advance_matches_numpy(tmp_path, seed, delta):
+    """qt::pcg_advance (the jump-ahead qt_stream_uniform uses) = numpy's PCG64.advance."""
+    (tmp_path / "a.cpp").write_text(ADV_SRC)
+    exe = tmp_path / "a"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(PKG, "csrc"), str(tmp_path / "a.cpp"), "-o",
+                    str(exe)], check=True)
+    out = subprocess.run([str(exe), str(seed), str(delta)], capture_output=True, text=True, check=True).stdout.split()
+    bg = np.random.default_rng(seed).bit_generator
+    bg.advance(delta)
+    np.testing.assert_array_equal(np.array([int(v) for v in out], dtype=np.uint64), bg.random_raw(4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("first,n", [(0, 1), (0, 1000), (131071, 4097), (262143, 1)])
+def test_device_stream_uniform_matches_numpy(first, n):
+    """qt_stream_uniform: draw vectors first.. of one default_rng stream, bitwise
+    numpy's uniform(lo, hi, size=(first + n, k))[first:]; the config-4 candidate
+    tensors equal the host candidate arrays."""
+    import torch
+
+    from quadtrack import core, workloads
+
+    lo, hi = [5e-5, 1e-3, 0.5, -2.0], [5e-4, 1e-2, 2.0, 3.0]
+    got = core.stream_uniform(42, first, n, lo, hi, torch.device("cuda", 0)).cpu().numpy()
+    bg = np.random.default_rng(42)
+    bg.bit_generator.advance(4 * first)
+    np.testing.assert_array_equal(got, bg.uniform(lo, hi, size=(n, 4)).T)
+    dev = [t.cpu().numpy() for t in workloads.tuner_candidate_tensors(first, first + n, torch.device("cuda", 0))]
+    for a, b in zip(dev, workloads.tuner_candidate_arrays(first, first + n)):
+        np.testing.assert_array_equal(a, b)
