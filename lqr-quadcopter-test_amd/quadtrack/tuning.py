@@ -311,6 +311,19 @@ def grid_configs(space: GainSearchSpace, points: int) -> list[dict]:
     return out
 
 
+def score_rows(ratio: np.ndarray, err: np.ndarray, succ: np.ndarray) -> list[tuple[float, dict]]:
+    """Per-candidate (score, metrics) from [C, E] episode metrics
+    (tuning.py:908-928): np.mean of each candidate's E values, score =
+    mean ratio - 0.1 * mean error.  One reduction per array: numpy reduces
+    each contiguous row of a C-ordered array exactly as it reduces that row
+    alone, so the values equal the reference's per-candidate np.mean."""
+    E = ratio.shape[1]
+    mean_on, mean_err, rate = (np.ascontiguousarray(a, dtype=np.float64).mean(axis=1) for a in (ratio, err, succ))
+    score = mean_on - 0.1 * mean_err
+    return [(s, {"mean_on_target_ratio": r, "mean_tracking_error": e, "success_rate": q, "episodes_evaluated": E})
+            for s, r, e, q in zip(score.tolist(), mean_on.tolist(), mean_err.tolist(), rate.tolist())]
+
+
 class BatchedTuner:
     """`ControllerTuner` with every candidate evaluated in one batch.
 
@@ -419,18 +432,8 @@ class BatchedTuner:
         from ._abi import MET
 
         C = len(configs)
-        ratio = m[MET["on_target_ratio"]].reshape(C, E)
-        err = m[MET["mean_tracking_error"]].reshape(C, E)
-        succ = m[MET["success"]].reshape(C, E)
-        out = []
-        for c in range(C):
-            mean_on = np.mean(list(ratio[c]))
-            mean_err = np.mean(list(err[c]))
-            rate = np.mean(list(succ[c]))
-            score = mean_on - 0.1 * mean_err
-            out.append((float(score), {"mean_on_target_ratio": float(mean_on), "mean_tracking_error": float(mean_err),
-                                       "success_rate": float(rate), "episodes_evaluated": E}))
-        return out
+        return score_rows(m[MET["on_target_ratio"]].reshape(C, E), m[MET["mean_tracking_error"]].reshape(C, E),
+                          m[MET["success"]].reshape(C, E))
 
     def _evaluate_config(self, controller_config: dict) -> tuple[float, dict]:
         """One candidate's (score, metrics), as tuning.py:846-928 returns them."""
@@ -486,5 +489,5 @@ class BatchedTuner:
 # the reference's class name (controllers/tuning.py:581): same constructor and tune()
 ControllerTuner = BatchedTuner
 
-__all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "ControllerTuner", "random_configs", "grid_configs",
+__all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "ControllerTuner", "score_rows", "random_configs", "grid_configs",
            "default_search_space"]

@@ -103,3 +103,24 @@ def test_controller_tuner_evaluate_config(tmp_path):
         score, metrics = t._evaluate_config(r["config"])
         assert score == pytest.approx(r["score"], rel=1e-8, abs=1e-10)
         assert metrics["mean_on_target_ratio"] == pytest.approx(r["metrics"]["mean_on_target_ratio"], rel=1e-8)
+
+
+def test_score_rows_equal_per_candidate_means():
+    """The vectorised candidate scores equal the reference's per-candidate
+    np.mean(list(...)) loop (tuning.py:908-928) bit for bit, for E below and
+    above numpy's 8-element pairwise leaf."""
+    import numpy as np
+
+    from quadtrack.tuning import score_rows
+
+    rng = np.random.default_rng(9)
+    for C, E in [(1, 1), (7, 5), (300, 8), (64, 13), (33, 130)]:
+        ratio = rng.integers(0, 3001, (C, E)) / 3000.0
+        err = rng.lognormal(size=(C, E))
+        succ = rng.integers(0, 2, (C, E)).astype(float)
+        got = score_rows(ratio, err, succ)
+        for c in range(C):
+            mean_on, mean_err, rate = np.mean(list(ratio[c])), np.mean(list(err[c])), np.mean(list(succ[c]))
+            assert got[c][0] == float(mean_on - 0.1 * mean_err)
+            assert got[c][1] == {"mean_on_target_ratio": float(mean_on), "mean_tracking_error": float(mean_err),
+                                 "success_rate": float(rate), "episodes_evaluated": E}
