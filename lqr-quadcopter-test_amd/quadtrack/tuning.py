@@ -407,7 +407,14 @@ class BatchedTuner:
             def vec(v):
                 v = np.asarray(v, float)
                 return np.full(3, float(v)) if v.ndim == 0 and key not in ("r_thrust", "r_rate") else v
-            return np.stack([vec(c.get(key, base)) for c in configs])
+            vals = [c.get(key, base) for c in configs]
+            try:  # one conversion of the whole column (every candidate the same shape)
+                arr = np.array(vals, dtype=float)
+            except ValueError:
+                arr = None
+            if arr is None or arr.ndim not in (1, 2) or (arr.ndim == 1 and key not in ("r_thrust", "r_rate")):
+                return np.stack([vec(v) for v in vals])
+            return arr
 
         kw = {k: col(k) for k in self._PER_CANDIDATE[kind] if k in keys}
         if kind == "riccati_lqr" and shared["use_lqi"]:
