@@ -43,6 +43,10 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, spec (half the FP32 vector 157
 HBM_PEAK_GBS = 8000.0
 # the dominant kernel of the bench workload: yaw-at-rest fast flavour, linear target, 6-column structured K
 KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true"
+# Warm-up floor: a fresh box's first ~0.5 s of passes run at lower clocks
+# (round 2: --warmup 5, 8 ms of GPU work, measured ~7% below --warmup 20), so
+# the warm-up runs for at least this long whatever --warmup says.
+WARMUP_FLOOR_S = 1.0
 
 
 def parse():
@@ -50,27 +54,59 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup-seconds", type=float, default=WARMUP_FLOOR_S,
+                    help="minimum warm-up time: passes are added after --warmup until this much has run")
     ap.add_argument("--episodes", type=int, default=65536, help="episodes per GPU")
     ap.add_argument("--motion", default="linear")
     ap.add_argument("--cpu-sample", type=int, default=65536, help="episodes in the CPU baseline sample (rank 0, N=1)")
     ap.add_argument("--cpu-sample-1core", type=int, default=4096, help="episodes of the 1-thread CPU sample")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the OpenMP CPU leg (0: see cpu_baseline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU plumbing check of the N-rank launch (gloo, no kernels): prints the ranks seen")
     return ap.parse_args()
 
 
+def visible_gpu_count() -> int:
+    """GPUs this process could open, counted without the HIP runtime (the
+    launcher parent must not load or initialise it before it starts the ranks):
+    KFD topology nodes with SIMDs whose DRM render node exists and is
+    accessible — the agents ROCr itself enumerates — narrowed by the
+    *_VISIBLE_DEVICES lists.  0 when there is no KFD (no ROCm GPU)."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return 0
+    n = 0
+    for node in nodes:
+        try:
+            props = dict(line.split(" ", 1) for line in open(os.path.join(base, node, "properties")).read().splitlines()
+                         if " " in line)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue
+        render = f"/dev/dri/renderD{int(props.get('drm_render_minor', '-1'))}"
+        if os.access(render, os.R_OK | os.W_OK):
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([d for d in v.split(",") if d.strip()]))
+    return n
+
+
 def launch(args) -> int:
     """Re-run this script as N ranks under torch.distributed.run (child
-    process, no exec; nothing here has touched the GPU)."""
+    process, no exec).  Nothing here imports torch or touches the HIP runtime:
+    the GPU count comes from the KFD topology (visible_gpu_count), and each
+    rank checks its own device again."""
     import socket
     import subprocess
 
     if not args.launcher_check:
-        import torch
-
-        visible = torch.cuda.device_count()  # a count, not a GPU initialisation
+        visible = visible_gpu_count()
         if visible < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) are visible", file=sys.stderr, flush=True)
             return 2
@@ -174,14 +210,37 @@ def main():
             pending.append(dist.all_reduce(part[0:5], async_op=True))
         return met
 
+    # warm-up: --warmup passes, then more until --warmup-seconds have run.  The
+    # extra count is agreed over ranks (MAX) so every rank issues the same
+    # number of per-pass all-reduces.
+    tw0 = time.perf_counter()
+    warm = 0
     for _ in range(args.warmup):
         one_pass(False)
+        warm += 1
+    torch.cuda.synchronize()
+    if args.warmup_seconds > 0:
+        t_probe = time.perf_counter()
+        for _ in range(5):
+            one_pass(False)
+        torch.cuda.synchronize()
+        warm += 5
+        per_pass = (time.perf_counter() - t_probe) / 5
+        extra = max(0, int(np.ceil((args.warmup_seconds - (time.perf_counter() - tw0)) / per_pass)))
+        if world > 1:
+            et = torch.tensor([extra], dtype=torch.int64, device=dev)
+            dist.all_reduce(et, op=dist.ReduceOp.MAX)
+            extra = int(et.item())
+        for _ in range(extra):
+            one_pass(False)
+        warm += extra
     for w in pending:
         w.wait()
     pending.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    warmup_s = time.perf_counter() - tw0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         met = one_pass(True)
@@ -266,6 +325,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_passes_run": warm,
+            "warmup_s": round(warmup_s, 3),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -362,7 +423,16 @@ def cpu_baseline(args, cfg, seeds, gpu_met):
 
     m1 = min(args.cpu_sample_1core, len(seeds))
     met1, dt1, _ = timed(m1, 1)
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    # threads: --cpu-threads, else OMP_NUM_THREADS (the GPU box sets it to 16, its CPU share per
+    # GPU, and asks that pools stay within it), else every CPU this process may run on
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if args.cpu_threads:
+        threads, why = args.cpu_threads, "--cpu-threads"
+    elif omp:
+        threads, why = omp, f"OMP_NUM_THREADS={omp} (the GPU box's CPU share per GPU)"
+    else:
+        threads, why = affinity, "sched_getaffinity"
     met, dt, used = timed(len(seeds), threads)
     steps = float(met[:, -1].sum())
     diff = float(np.max(np.abs(gpu_met.cpu().numpy().T - met)))
@@ -371,7 +441,7 @@ def cpu_baseline(args, cfg, seeds, gpu_met):
                      f"OpenMP over episodes, {int(used)} threads), {dt:.2f} s wall",
            "single_core": {"value": round(float(met1[:, -1].sum()) / dt1, 1), "cores": 1,
                            "sample": f"first {m1} episodes x 3000 steps, 1 thread, {dt1:.2f} s wall"},
-           "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+           "threads_source": why, "affinity_cpus": affinity, "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
     return cpu, diff
 
 

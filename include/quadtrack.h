@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 6
+#define QT_ABI_VERSION 7
 
 /* error codes */
 #define QT_OK 0
@@ -237,6 +237,18 @@ int qt_stream_uniform(uint64_t seed, int64_t first, int64_t n, int32_t k, const 
    rec[((s*16 + j) * n) + e] for j < 12 and the applied controller action at j = 12..15. */
 int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, void* stream);
+
+/* ABI 7.  qt_rollout with the env's per-step rewards kept, for the trainer's
+   classical evaluation epoch (train.py:578-652, which the reference runs one
+   env.step at a time): reward[0][e] += env.step's reward, -(post-step tracking
+   error) (quadcopter_env.py:198-199, 498-511), in step order (the trainer's
+   sum(), train.py:627); reward[1][e] = the last step's post-step tracking
+   error (info["tracking_error"], train.py:630).  Its on-target ratio
+   (info["on_target_ratio"]) is acc[QT_ACC_ON_POST] / acc[QT_ACC_STEPS].
+   reward[2][n] is read and written (zero it before the first chunk).  Runs the
+   exact step; `motion` / `order` batches as qt_rollout. */
+int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                       const qt_batch* batch, qt_state st, int32_t nsteps, double* reward, void* stream);
 
 /* qt_rollout for a batch of mixed motion types without per-step motion
    dispatch.  batch->order must list the episodes grouped by motion: slots

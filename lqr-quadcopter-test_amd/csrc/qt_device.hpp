@@ -12,7 +12,7 @@
 #include <stdint.h>
 
 #include "../../include/quadtrack.h"
-#include "qt_crtrig.hpp"
+#include "qt_glibc.hpp"
 #include "qt_math.hpp"
 
 namespace qt {
@@ -50,7 +50,7 @@ __device__ __forceinline__ bool same_sign(double a, double b) {
 // Per-episode constants of a motion pattern, precomputed once per launch.
 struct Pattern {
   double c0, c1, c2;  // linear: velocity xyz | circular: theta0, omega | sinusoidal: phases
-  double o0, o1, o2;  // sinusoidal: omegas | figure8: omega
+  double o0, o1, o2;  // sinusoidal: omegas | figure8: omega | circular: pow(omega, 2)
 };
 
 // TargetMotion._create_pattern + pattern constructors (target_motion.py:306-369,
@@ -69,6 +69,7 @@ __device__ __forceinline__ Pattern make_pattern(const qt_env_params& e, int moti
   } else if (motion == QT_MOTION_CIRCULAR) {
     p.c0 = r0;
     p.c1 = e.speed / e.radius;
+    p.o0 = glibc::pow2(p.c1);  // omega**2 of a Python float: libm pow (target_motion.py:107)
   } else if (motion == QT_MOTION_SINUSOIDAL) {
     p.c0 = r0;
     p.c1 = r1;
@@ -104,8 +105,8 @@ __device__ __forceinline__ void periodic_state(const qt_env_params& e, int motio
     v[0] = -r * om * s[0];
     v[1] = r * om * c[0];
     v[2] = 0.0;
-    a[0] = WANT_ACC ? -r * (om * om) * c[0] : 0.0;
-    a[1] = WANT_ACC ? -r * (om * om) * s[0] : 0.0;
+    a[0] = WANT_ACC ? -r * pt.o0 * c[0] : 0.0;
+    a[1] = WANT_ACC ? -r * pt.o0 * s[0] : 0.0;
     a[2] = 0.0;
   } else {
     const double amp[3] = {e.amplitude, e.amplitude * 0.5, e.amplitude * 0.25};
@@ -195,20 +196,21 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
   } else if (motion == QT_MOTION_FIGURE8) {
     // With the acceleration wanted (feed-forward) the forward difference
     // below multiplies the positions' last bit by ~1e12, so they are formed
-    // as numpy forms them: sin / cos correctly rounded (cr_sincos; glibc's,
-    // the reference's, round correctly but for ~0.15% of arguments) and no
-    // FMA contraction (1 + sin^2 contracted is not 1 + fl(sin^2)).
+    // exactly as numpy forms them: glibc's sin / cos and pow(x, 2)
+    // (qt_glibc.hpp, bitwise the host libm) and no FMA contraction.
 #pragma clang fp contract(off)
     const double sc = e.amplitude, om = pt.o0;
     double st, ct;
-    if (WANT_ACC)
-      cr_sincos(om * t, &st, &ct);
-    else
+    if (WANT_ACC) {
+      ct = glibc::cos(om * t);
+      st = glibc::sin(om * t);
+    } else {
       fast_sincos(om * t, &st, &ct);
-    double den = 1.0 + st * st;
-    double dcos = -st * om, dsin = ct * om;
-    double dden = 2.0 * st * dsin;
-    double den2 = den * den;
+    }
+    const double den = 1.0 + (WANT_ACC ? glibc::pow2(st) : st * st);
+    const double dcos = -st * om, dsin = ct * om;
+    const double dden = 2.0 * st * dsin;
+    const double den2 = WANT_ACC ? glibc::pow2(den) : den * den;
     const double p0 = e.center[0] + sc * ct / den;
     const double p1 = e.center[1] + sc * st * ct / den;
     const double v0 = sc * ((dcos * den - ct * dden) / den2);
@@ -217,11 +219,11 @@ __device__ __forceinline__ void target_state(const qt_env_params& e, int motion,
     if (WANT_ACC) {
       // the reference's 1e-6 forward difference (target_motion.py:215-229)
       const double h = 1e-6;
-      double stp, ctp;
-      cr_sincos(om * (t + h), &stp, &ctp);
-      double denp = 1.0 + stp * stp;
-      double pp0 = e.center[0] + sc * ctp / denp;
-      double pp1 = e.center[1] + sc * stp * ctp / denp;
+      const double thp = om * (t + h);
+      const double ctp = glibc::cos(thp), stp = glibc::sin(thp);
+      const double denp = 1.0 + glibc::pow2(stp);
+      const double pp0 = e.center[0] + sc * ctp / denp;
+      const double pp1 = e.center[1] + sc * stp * ctp / denp;
       a0 = ((pp0 - p0) / h - v0) / h;
       a1 = ((pp1 - p1) / h - v1) / h;
     }
@@ -492,6 +494,9 @@ struct LaunchConst {
   // `epoch` there; the exact pass returns at once unless it reads its epoch
   unsigned long long* defer_flag;
   unsigned long long epoch;
+  // qt_rollout_rewards (exact step only): [2][n] reward sum and last
+  // post-step tracking error, accumulated across launches; null otherwise
+  double* reward;
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)

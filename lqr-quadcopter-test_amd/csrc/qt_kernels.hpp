@@ -175,7 +175,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
                                           const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
                                           Target& tg, double& t, Acc& a, int nsteps, double* __restrict__ rec,
-                                          int64_t n, int64_t ep) {
+                                          int64_t n, int64_t ep, double* __restrict__ reward = nullptr) {
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
@@ -190,6 +190,11 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
   if constexpr (kCarry) periodic_trig_init(pt, t, ptrig);
+  // env.step's reward = -(post-step tracking error) (quadcopter_env.py:198-199,
+  // 498-511), summed in step order as the trainer does (train.py:627), and the
+  // last step's tracking error (info["tracking_error"], train.py:630)
+  double rew_sum = 0.0, rew_last = 0.0;
+  if (!FAST && reward) rew_sum = reward[ep], rew_last = reward[n + ep];
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -268,6 +273,11 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
+      if (reward) {
+        const double pe = sqrt(dot3_blas(q0, q1, q2));  // float(np.linalg.norm(quad_pos - target_pos))
+        rew_sum += -pe;
+        rew_last = pe;
+      }
       if (QT_ABLATE & QT_ABL_TERMINATION)
         a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
       else
@@ -282,6 +292,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       }
     }
   }
+  if (!FAST && reward) reward[ep] = rew_sum, reward[n + ep] = rew_last;
 }
 
 // Finiteness by the exponent bits: the same answer under IEEE and under the
@@ -662,7 +673,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   } else {
     if (deferred != kExact && wave_ok) return;
     run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec, n,
-                                         ep);
+                                         ep, lc.reward);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
   // feed-forward reads them); the stored observation carries the reference's

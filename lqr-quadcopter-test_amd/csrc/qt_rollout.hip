@@ -605,7 +605,9 @@ unsigned long long* defer_flag_for(hipStream_t s) {
   if (it != flags.end()) return it->second;
   unsigned long long* f = nullptr;
   if (hipMalloc(&f, sizeof(*f)) != hipSuccess) return nullptr;
-  if (hipMemset(f, 0, sizeof(*f)) != hipSuccess) {  // epoch 0 is never issued
+  // zeroed on `s` itself: ordered before the first fast launch that writes it
+  // there (a null-stream memset is not ordered with non-blocking streams)
+  if (hipMemsetAsync(f, 0, sizeof(*f), s) != hipSuccess) {  // epoch 0 is never issued
     (void)hipFree(f);
     return nullptr;
   }
@@ -626,11 +628,13 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 // it in one launch (rollout_grouped_kernel), the exact pass with runtime motion.
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
-                   double* rec, bool grouped = false) {
+                   double* rec, bool grouped = false, double* reward = nullptr) {
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
+  lc.reward = reward;
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
-  const int flavor = flavor_for(kc, ks, no_yaw, e, c, rec);
+  // rewards are accumulated by the exact step only
+  const int flavor = reward ? kExact : flavor_for(kc, ks, no_yaw, e, c, rec);
   if (flavor != kExact) {
     lc.defer_flag = defer_flag_for(s);  // null (no flag: the exact pass tests every wave) if unavailable
     lc.epoch = g_defer_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
@@ -694,6 +698,19 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
   return launch_rollout(batch->k_cols, ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+}
+
+int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                       const qt_batch* batch, qt_state st, int32_t nsteps, double* reward, void* stream) {
+  if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
+  if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (batch->n == 0 || nsteps == 0) return QT_OK;
+  if (!reward || !valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
+  const BatchDev b = to_dev(batch);
+  const int motion = batch->motion ? -1 : env->motion;
+  const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;
+  return launch_rollout(batch->k_cols, ff, batch->k_structured != 0, batch->k_no_yaw != 0, motion, grid_of(batch->n),
+                        (hipStream_t)stream, *env, *ctrl, *crit, b, st, nsteps, nullptr, false, reward);
 }
 
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,

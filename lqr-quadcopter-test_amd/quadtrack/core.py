@@ -279,6 +279,22 @@ def rollout(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatc
                                  int(nsteps), ptr(rec), stream_of(batch.device)), "qt_rollout")
 
 
+def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState,
+                    nsteps: int, reward: torch.Tensor):
+    """qt_rollout_rewards: the exact-step rollout that also accumulates
+    reward[0] += -(post-step tracking error) per step and keeps the last one in
+    reward[1] (reward: float64 [2, n], zeroed before the first chunk)."""
+    lib = _abi.load()
+    if reward.dtype != F64 or not reward.is_contiguous() or tuple(reward.shape) != (2, batch.n):
+        raise ValueError("reward must be a contiguous float64 [2, n] tensor")
+    if batch.groups is not None:
+        raise ValueError("rollout_rewards takes an ungrouped batch (motion per episode is fine)")
+    with torch.cuda.device(batch.device):
+        check(lib.qt_rollout_rewards(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()),
+                                     st.c_state(), int(nsteps), ptr(reward), stream_of(batch.device)),
+              "qt_rollout_rewards")
+
+
 def motion_groups(motion: np.ndarray):
     """Host grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end)."""
     motion = np.asarray(motion).reshape(-1)

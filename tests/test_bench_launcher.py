@@ -65,3 +65,47 @@ def test_more_gpus_than_visible_is_an_error():
     assert r.returncode == 2
     assert "GPU(s) are visible" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+_PARENT_PROBE = r"""
+import json, subprocess, sys
+sys.path.insert(0, {root!r})
+import bench
+
+def fake_call(cmd, env=None):
+    maps = open("/proc/self/maps").read()
+    print(json.dumps({{"hip_mapped": "libamdhip64" in maps, "torch_loaded": "torch" in sys.modules,
+                      "cmd_has_run": "torch.distributed.run" in cmd}}), flush=True)
+    return 0
+
+subprocess.call = fake_call
+bench.visible_gpu_count = lambda: {fake_gpus}
+sys.argv = ["bench.py"] + {argv!r}
+bench.main()
+"""
+
+
+@pytest.mark.parametrize("argv", [["--gpus", "2", "--launcher-check"], ["--gpus", "8", "--steps", "1"]])
+def test_launcher_parent_never_loads_hip(argv):
+    """The parent that starts the ranks reads no HIP: at the moment it would
+    spawn torch.distributed.run, libamdhip64 is not mapped and torch is not
+    imported (the GPU count comes from the KFD topology)."""
+    code = _PARENT_PROBE.format(root=ROOT, fake_gpus=8, argv=argv)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=_env(), timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line == {"hip_mapped": False, "torch_loaded": False, "cmd_has_run": True}
+
+
+def test_visible_gpu_count_without_hip():
+    """visible_gpu_count reads sysfs only: no torch import, and it honours
+    HIP_VISIBLE_DEVICES narrowing."""
+    code = ("import sys, os; sys.path.insert(0, %r); import bench; n = bench.visible_gpu_count(); "
+            "os.environ['HIP_VISIBLE_DEVICES'] = '0'; m = bench.visible_gpu_count(); "
+            "print(n, m, 'torch' in sys.modules)") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=_env(), timeout=60)
+    n, m, torch_loaded = r.stdout.split()
+    assert torch_loaded == "False"
+    assert int(m) == min(int(n), 1)
+    if not gpu_available():
+        assert int(n) == 0

@@ -1,0 +1,63 @@
+"""The trainer's classical evaluation epoch (quadtrack.train.evaluate_epoch,
+one qt_rollout_rewards launch per epoch) against the reference's own
+Trainer._evaluate_epoch (train.py:578-652), run by
+tests/golden/gen_trainer.py into trainer_epochs.json: per-episode reward sums,
+last-step info on-target ratios and tracking errors, step counts (exact), and
+the epoch means.
+
+Tolerance: 1e-8 relative (and 1e-8 absolute) on every value — the
+trajectories differ from the reference's only by the DARE gains' sub-ulp
+difference (scipy QZ vs the doubling algorithm) — and step counts and
+on-target ratios (integer counts) exactly."""
+
+import json
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+FIX = json.load(open(os.path.join(GOLDEN, "trainer_epochs.json")))["scenarios"]
+CASES = [(s, e) for s in FIX for e in s["results"]]
+
+
+@pytest.mark.parametrize("s,ep", CASES, ids=[f"{s['name']}-epoch{e['epoch']}" for s, e in CASES])
+def test_evaluate_epoch_matches_reference_trainer(s, ep):
+    from quadtrack import _abi
+    from quadtrack.train import evaluate_epoch
+
+    _abi.require_gpu()
+    cfg = SimpleNamespace(controller=s["controller"], episodes_per_epoch=s["episodes_per_epoch"],
+                          max_steps_per_episode=s["max_steps_per_episode"], env_seed=s["env_seed"],
+                          target_motion_type=s["motion"], episode_length=s["episode_length"],
+                          target_radius=s["target_radius"], full_config={s["controller"]: s["ctl"]})
+    r = evaluate_epoch(cfg, epoch=ep["epoch"])
+    np.testing.assert_array_equal(r.episode_steps.cpu().numpy(), ep["episode_steps"])
+    np.testing.assert_array_equal(r.episode_on_target_ratio.cpu().numpy(), ep["episode_on_target_ratio"])
+    np.testing.assert_allclose(r.episode_reward.cpu().numpy(), ep["episode_reward"], rtol=1e-8, atol=1e-8)
+    np.testing.assert_allclose(r.episode_tracking_error.cpu().numpy(), ep["episode_tracking_error"], rtol=1e-8,
+                               atol=1e-8)
+    got = r.as_dict()
+    assert got["difficulty"] == 1.0
+    assert got["mean_on_target_ratio"] == ep["result"]["mean_on_target_ratio"]
+    for k in ("mean_reward", "mean_tracking_error"):
+        np.testing.assert_allclose(got[k], ep["result"][k], rtol=1e-8, atol=1e-8, err_msg=k)
+
+
+def test_evaluate_epoch_means_are_numpy_means():
+    """The epoch means are np.mean of the per-episode values, bit for bit
+    (qt_summary_numpy), at 10 episodes (numpy's 8-accumulator leaf) and 37."""
+    from quadtrack import _abi
+    from quadtrack.train import evaluate_epoch
+
+    _abi.require_gpu()
+    for n in (10, 37):
+        r = evaluate_epoch(controller="riccati_lqr", episodes_per_epoch=n, max_steps_per_episode=200,
+                           target_motion_type="sinusoidal", env_seed=5)
+        assert r.mean_reward == float(np.mean(r.episode_reward.cpu().numpy()))
+        assert r.mean_on_target_ratio == float(np.mean(r.episode_on_target_ratio.cpu().numpy()))
+        assert r.mean_tracking_error == float(np.mean(r.episode_tracking_error.cpu().numpy()))

@@ -246,3 +246,147 @@ def test_cr_sincos_vs_glibc(cr_probe):
     fin = np.isfinite(x)
     assert np.all(np.abs(s - np.sin(x))[fin] <= np.spacing(np.abs(np.sin(x)))[fin])
     assert np.isnan(cr_probe(np.array([np.inf, -np.inf, np.nan]))).all()
+
+
+# ------------------------------------------------ glibc sin / cos / pow(x, 2)
+# qt_glibc.hpp restates glibc 2.35's __sin_fma / __cos_fma / __ieee754_pow_fma
+# (the variants numpy's scalar np.sin / np.cos / x**2 reach on an FMA host) for
+# the figure-8 feed-forward target.  The probe evaluates both the host libm and
+# the restatement on the same arguments and counts bit mismatches.
+
+GLIBC_SRC = r"""
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "qt_glibc.hpp"
+extern "C" double sin(double);
+extern "C" double cos(double);
+extern "C" double pow(double, double);
+static bool same(double a, double b) {
+  uint64_t x, y;
+  memcpy(&x, &a, 8);
+  memcpy(&y, &b, 8);
+  return x == y || (a != a && b != b);
+}
+// splitmix64: arguments are generated here (1e7+ is too many to pass through files)
+static uint64_t sm(uint64_t& s) {
+  uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+int main(int argc, char** argv) {
+  long n = atol(argv[1]);
+  uint64_t seed = strtoull(argv[2], 0, 10);
+  long bad[3] = {0, 0, 0}, checked = 0;
+  std::vector<double> xs;
+  if (argc > 3) {  // explicit arguments from a file
+    FILE* f = fopen(argv[3], "rb");
+    double v;
+    while (fread(&v, 8, 1, f) == 1) xs.push_back(v);
+    fclose(f);
+    n = (long)xs.size();
+  }
+  for (long i = 0; i < n; ++i) {
+    double x;
+    if (!xs.empty()) {
+      x = xs[i];
+    } else {
+      const uint64_t r = sm(seed);
+      const double u = (double)(r >> 11) * 0x1p-53;
+      switch (i % 8) {
+        case 0: x = (2 * u - 1) * 8.0; break;             // a few periods: every quadrant / table entry
+        case 1: x = (2 * u - 1) * 200.0; break;           // figure-8 angles omega t over long episodes
+        case 2: x = std::ldexp(1.0 + u, -30 + (int)(u * 30)); break;  // small: Taylor / tiny branches
+        case 3: x = 0.8 + u * 1.7; break;                 // the hp0 - |x| branch
+        case 4: x = (2 * u - 1) * 1e7; break;             // large reduce_sincos arguments
+        case 5: { const uint64_t b = sm(seed); memcpy(&x, &b, 8); break; }  // any bit pattern
+        case 6: x = (2 * u - 1) * 2.0; break;             // sin_t and 1 + sin_t^2 of the figure-8
+        default: x = std::ldexp(u, -1074 + (int)(u * 2100)); break;   // subnormals .. huge (pow)
+      }
+    }
+    const bool trig = std::fabs(x) < 105414350.0 || !std::isfinite(x);
+    if (trig) {
+      bad[0] += !same(sin(x), qt::glibc::sin(x));
+      bad[1] += !same(cos(x), qt::glibc::cos(x));
+      ++checked;
+    }
+    bad[2] += !same(pow(x, 2.0), qt::glibc::pow2(x));
+  }
+  printf("%ld %ld %ld %ld %ld\n", n, checked, bad[0], bad[1], bad[2]);
+  return 0;
+}
+"""
+
+
+def _host_has_fma():
+    try:
+        return " fma " in open("/proc/cpuinfo").read().replace("\n", " ")
+    except OSError:
+        return False
+
+
+@pytest.fixture(scope="module")
+def glibc_probe(tmp_path_factory):
+    if not _host_has_fma():
+        pytest.skip("host libm would run its non-FMA variants, which qt_glibc.hpp does not restate")
+    d = tmp_path_factory.mktemp("glibc")
+    (d / "p.cpp").write_text(GLIBC_SRC)
+    exe = d / "p"
+    # -fno-builtin: every sin / cos / pow call goes to libm (no folding, no sincos merge, no pow(x, 2) -> x * x)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin", "-I", os.path.join(PKG, "csrc"),
+                    str(d / "p.cpp"), "-o", str(exe), "-lm"], check=True)
+
+    def run(n=0, seed=1, x=None):
+        args = [str(exe), str(n), str(seed)]
+        if x is not None:
+            (d / "in.bin").write_bytes(np.ascontiguousarray(x, dtype=np.float64).tobytes())
+            args.append(str(d / "in.bin"))
+        out = subprocess.run(args, check=True, capture_output=True, text=True).stdout.split()
+        return [int(v) for v in out]
+
+    return run
+
+
+def test_glibc_sin_cos_pow2_bitwise_vs_host_libm(glibc_probe):
+    """1.2e7 arguments over every branch of sin / cos (Taylor, table, hp0 - |x|,
+    reduce_sincos) and pow(x, 2) (subnormal to overflow, negative, +-0,
+    inf / nan): bitwise equal to the host glibc."""
+    n, checked, bs, bc, bp = glibc_probe(12_000_000, seed=20261017)
+    assert checked > 0.85 * n
+    assert (bs, bc, bp) == (0, 0, 0)
+
+
+def test_glibc_edge_arguments(glibc_probe):
+    """Branch boundaries (2^-27, 2^-26, 0.126, 0.855469, 2.426265, 105414350),
+    multiples of pi/4 and pi/2 (quadrant edges), the table grid i/128 and its
+    midpoints, and pow's special inputs."""
+    edges = []
+    for b in (2.0 ** -27, 2.0 ** -26, 0.126, 0.85546875, 2.426265, 105414349.0, 1.0, 0.5):
+        for v in (b, np.nextafter(b, 0), np.nextafter(b, np.inf)):
+            edges += [v, -v]
+    k = np.arange(-4000, 4001)
+    grid = np.arange(0, 112) / 128.0
+    x = np.concatenate([edges, k * (np.pi / 4), k * (np.pi / 2), np.nextafter(k * (np.pi / 2), np.inf),
+                        grid, grid + 1 / 256.0, -grid,
+                        [0.0, -0.0, 5e-324, -5e-324, 2.2250738585072014e-308, 1.7976931348623157e308,
+                         -1.7976931348623157e308, 1e154, 1.4e154, 1e-160, 1e-170, np.inf, -np.inf, np.nan]])
+    n, checked, bs, bc, bp = glibc_probe(x=x)
+    assert n == x.size and (bs, bc, bp) == (0, 0, 0)
+
+
+def test_glibc_is_what_numpy_scalars_call(glibc_probe):
+    """The reference's call forms themselves: np.sin / np.cos of a Python float
+    and np.float64 ** 2 (target_motion.py:178-180) agree with the host libm,
+    so the probe above compares against the right functions."""
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-60, 60, 3000), rng.uniform(-1.5, 1.5, 3000)])
+    import math  # math.sin / math.cos / math.pow call the host libm directly
+
+    for x in xs:
+        xf = float(x)
+        assert np.cos(xf) == math.cos(xf) and np.sin(xf) == math.sin(xf)
+        v = np.float64(xf)
+        assert v ** 2 == math.pow(xf, 2.0)
