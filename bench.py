@@ -210,30 +210,30 @@ def main():
             pending.append(dist.all_reduce(part[0:5], async_op=True))
         return met
 
-    # warm-up: --warmup passes, then more until --warmup-seconds have run.  The
-    # extra count is agreed over ranks (MAX) so every rank issues the same
-    # number of per-pass all-reduces.
+    # warm-up: --warmup passes, then chunks of ~0.1 s until --warmup-seconds
+    # have run.  Whether to go on is agreed over ranks (MAX) after each chunk,
+    # so every rank issues the same number of per-pass all-reduces.
     tw0 = time.perf_counter()
     warm = 0
     for _ in range(args.warmup):
         one_pass(False)
         warm += 1
     torch.cuda.synchronize()
-    if args.warmup_seconds > 0:
-        t_probe = time.perf_counter()
-        for _ in range(5):
+    chunk = 5
+    while args.warmup_seconds > 0:
+        go = time.perf_counter() - tw0 < args.warmup_seconds
+        if world > 1:
+            gt = torch.tensor([int(go)], dtype=torch.int64, device=dev)
+            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+            go = bool(gt.item())
+        if not go:
+            break
+        tc = time.perf_counter()
+        for _ in range(chunk):
             one_pass(False)
         torch.cuda.synchronize()
-        warm += 5
-        per_pass = (time.perf_counter() - t_probe) / 5
-        extra = max(0, int(np.ceil((args.warmup_seconds - (time.perf_counter() - tw0)) / per_pass)))
-        if world > 1:
-            et = torch.tensor([extra], dtype=torch.int64, device=dev)
-            dist.all_reduce(et, op=dist.ReduceOp.MAX)
-            extra = int(et.item())
-        for _ in range(extra):
-            one_pass(False)
-        warm += extra
+        warm += chunk
+        chunk = max(1, min(1000, int(0.1 / max((time.perf_counter() - tc) / chunk, 1e-6))))
     for w in pending:
         w.wait()
     pending.clear()
@@ -256,7 +256,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_all = np.array([a.elapsed_time(b) for a, b in ev])
+    kern_ms = float(np.mean(kern_all))
     steps_done = met[core._abi.MET["steps"]].sum()
     local_env_steps = float(steps_done.item())  # this rank's executed env-steps per pass
     per_rank = [local_env_steps]
@@ -345,6 +346,8 @@ def main():
                          "kernel": "rollout_kernel<yaw-at-rest fast step, LINEAR, K=6, no-FF, structured K> "
                                    "+ its deferred exact pass (HIP events around both)",
                          "kernel_ms": round(kern_ms, 4),
+                         "kernel_ms_min_median_max": [round(float(v), 4) for v in
+                                                      (kern_all.min(), np.median(kern_all), kern_all.max())],
                          "flops_per_env_step": FLOPS_PER_ENV_STEP,
                          "profiled": prof_line},
             "ranks": {"world_size_seen": seen, "backend": "nccl (RCCL)" if world > 1 else None,

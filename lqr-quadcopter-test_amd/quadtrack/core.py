@@ -213,10 +213,6 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
             raise ValueError(f"{name} must have {n} contiguous entries")
     if batch.motion is not None and (int(batch.motion.min()) < 0 or int(batch.motion.max()) > 4):
         raise ValueError("motion types must be in 0..4")
-    if batch.order is not None:
-        o = batch.order.to(torch.int64)
-        if int(o.min()) < 0 or int(o.max()) >= n:
-            raise ValueError("order entries out of range")
     if st is not None:
         _check_cols("x", st.x, 12, n)
         _check_cols("integ", st.integ, INTEG_ROWS, n)
@@ -233,8 +229,18 @@ def validate(batch: EpisodeBatch, st: RolloutState | None = None):
     if batch.order is not None:
         if batch.order.dtype != torch.int32 or batch.order.device != batch.device:
             raise ValueError("order must be an int32 tensor on the batch device")
-        if torch.unique(batch.order).numel() != n:
-            raise ValueError("order must be a permutation of the episodes")
+        if n:
+            # the kernels index st.x[i * n + order[slot]]: a permutation of 0..n-1, checked
+            # with one bincount (no sort) and one host read
+            o = batch.order.to(torch.int64)
+            lo, hi = o.min(), o.max()
+            ok = (lo >= 0) & (hi < n)
+            perm = ok & (torch.bincount(o.clamp(0, n - 1), minlength=n) == 1).all()
+            ok, perm = (bool(v) for v in torch.stack([ok, perm]).tolist())
+            if not ok:
+                raise ValueError("order entries out of range")
+            if not perm:
+                raise ValueError("order must be a permutation of the episodes")
 
 
 def seed_draws(seeds: torch.Tensor, motion: torch.Tensor | None, motion_default: int):

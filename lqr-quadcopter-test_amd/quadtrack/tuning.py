@@ -337,6 +337,9 @@ class BatchedTuner:
                 import cma  # noqa: F401
             except ImportError:
                 raise ImportError("CMA-ES strategy requires the 'cma' package. Install it with: pip install cma")
+            # with cma installed the reference runs its sequential ask / tell loop; that
+            # search strategy is not batched here, so refuse it up front
+            raise NotImplementedError("CMA-ES is a sequential search; the batched tuner runs grid and random")
         self.config = config
         self.device = device
         self.base = dict(base_controller_config or {})
@@ -369,50 +372,83 @@ class BatchedTuner:
         return SuccessCriteria(min_on_target_ratio=0.8, min_episode_duration=self.config.episode_length,
                                target_radius=self.config.target_radius)
 
-    # per-candidate keys each controller type reads (its constructor's per-episode arrays)
+    # per-candidate keys each controller type reads (its batched constructor's per-episode arrays)
     _PER_CANDIDATE = {
-        "riccati_lqr": ("q_pos", "q_vel", "r_controls", "q_int"),
-        "pid": ("kp_pos", "ki_pos", "kd_pos"),
-        "lqr": ("q_pos", "q_vel", "r_thrust", "r_rate"),
+        "riccati_lqr": ("q_pos", "q_vel", "r_controls", "q_int", "mass"),
+        "pid": ("kp_pos", "ki_pos", "kd_pos", "mass"),
+        "lqr": ("q_pos", "q_vel", "r_thrust", "r_rate", "mass"),
     }
     _FF_KEYS = ("ff_velocity_gain", "ff_acceleration_gain")
+    # PIDController reads config.get("kp_pos", config.get("kp", default)) (controllers/__init__.py)
+    _ALIASES = {"pid": {"kp": "kp_pos", "ki": "ki_pos", "kd": "kd_pos"}}
+
+    @classmethod
+    def _canonical(cls, kind: str, cfg: dict) -> dict:
+        """A candidate with the controller's key aliases resolved as its
+        constructor resolves them (the canonical key wins over its alias)."""
+        out = dict(cfg)
+        for alias, key in cls._ALIASES.get(kind, {}).items():
+            if alias in out:
+                v = out.pop(alias)
+                out.setdefault(key, v)
+        return out
 
     def controller(self, configs: list[dict]):
         """One batched controller over the candidates, one gain set (one DARE
-        for riccati_lqr) per candidate (tuning.py:832-844)."""
+        for riccati_lqr) per candidate, built from each candidate's whole
+        config as the reference builds one controller per candidate
+        (tuning.py:832-844): keys with a per-candidate form become arrays,
+        any other key must be the same for every candidate and joins the
+        shared config (a key that varies without a per-candidate form
+        raises)."""
         kind = self.config.controller_type
+        base = self._canonical(kind, self.base)
+        configs = [self._canonical(kind, c) for c in configs]
         keys = set().union(*[c.keys() for c in configs]) if configs else set()
-        shared = dict(self.base)
+        shared = dict(base)
         if kind == "riccati_lqr":
-            lqi = {bool(c.get("use_lqi", False)) for c in configs}
+            lqi = {bool(c.get("use_lqi", base.get("use_lqi", False))) for c in configs}
             if len(lqi) > 1:
                 raise ValueError("candidates mix LQR and LQI")
             shared["use_lqi"] = lqi.pop() if lqi else False
-        if any(c.get("feedforward_enabled") for c in configs):
+        if any(c.get("feedforward_enabled", base.get("feedforward_enabled")) for c in configs):
             shared["feedforward_enabled"] = True
+        per = set(self._PER_CANDIDATE[kind]) | set(self._FF_KEYS)
+        _missing = object()
+        for key in sorted(keys - per - {"use_lqi", "feedforward_enabled"}):
+            vals = [c.get(key, base.get(key, _missing)) for c in configs]
+            first = vals[0]
+            same = all(v is not _missing for v in vals) and all(
+                np.array_equal(np.asarray(v, dtype=object), np.asarray(first, dtype=object)) for v in vals[1:])
+            if not same:
+                raise ValueError(f"candidate key '{key}' differs between candidates and has no per-candidate "
+                                 f"form in the batched {kind} controller")
+            shared[key] = first
 
         defaults = {"q_pos": [1e-4, 1e-4, 16.0], "q_vel": [0.0036, 0.0036, 4.0], "r_controls": [1.0] * 4,
                     "q_int": [0.0, 0.0, 0.0], "r_thrust": 1.0, "r_rate": 1.0,
                     "ff_velocity_gain": [0.0, 0.0, 0.0], "ff_acceleration_gain": [0.0, 0.0, 0.0]}
+        scalar_keys = ("r_thrust", "r_rate", "mass")
 
         def col(key):
             if kind == "pid" and key in ("kp_pos", "ki_pos", "kd_pos"):
                 from .controllers.pid import _DEFAULT_KD, _DEFAULT_KI, _DEFAULT_KP
                 d = {"kp_pos": _DEFAULT_KP, "ki_pos": _DEFAULT_KI, "kd_pos": _DEFAULT_KD}[key]
-                alt = key[:2]
-                base = shared.get(key, shared.get(alt, d))
+                base_v = shared.get(key, d)
+            elif key == "mass":
+                base_v = shared.get("mass", 1.0)
             else:
-                base = shared.get(key, defaults[key])
+                base_v = shared.get(key, defaults[key])
 
             def vec(v):
                 v = np.asarray(v, float)
-                return np.full(3, float(v)) if v.ndim == 0 and key not in ("r_thrust", "r_rate") else v
-            vals = [c.get(key, base) for c in configs]
+                return np.full(3, float(v)) if v.ndim == 0 and key not in scalar_keys else v
+            vals = [c.get(key, base_v) for c in configs]
             try:  # one conversion of the whole column (every candidate the same shape)
                 arr = np.array(vals, dtype=float)
             except ValueError:
                 arr = None
-            if arr is None or arr.ndim not in (1, 2) or (arr.ndim == 1 and key not in ("r_thrust", "r_rate")):
+            if arr is None or arr.ndim not in (1, 2) or (arr.ndim == 1 and key not in scalar_keys):
                 return np.stack([vec(v) for v in vals])
             return arr
 
@@ -494,6 +530,10 @@ class BatchedTuner:
 
 
 # the reference's class name (controllers/tuning.py:581): same constructor and tune()
+# for grid and random search.  Differences: strategy "cma_es"
+# raises (ImportError without `cma`, as the reference; NotImplementedError with
+# it), and there is no SIGINT / SIGTERM partial save (the whole search is one
+# batch), so TuningResult.interrupted is always False.
 ControllerTuner = BatchedTuner
 
 __all__ = ["GainSearchSpace", "TuningConfig", "TuningResult", "BatchedTuner", "ControllerTuner", "score_rows", "random_configs", "grid_configs",

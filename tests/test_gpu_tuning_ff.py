@@ -147,3 +147,50 @@ def test_per_episode_ff_off_equals_no_ff(qt):
     b = run_closed_loop(withff, env_cfg, n=n, seeds=np.arange(n), max_steps=500)
     np.testing.assert_allclose(b.metrics.cpu().numpy(), a.metrics.cpu().numpy(), rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(b.state.x.cpu().numpy(), a.state.x.cpu().numpy(), rtol=1e-12, atol=1e-12)
+
+
+CAND_EXTRA = {
+    # mass varies per candidate (a per-candidate array: DARE model + hover thrust), max_thrust is common
+    "riccati_lqr": [{"q_pos": [2e-4, 2e-4, 14.0], "mass": 1.2, "max_thrust": 18.0},
+                    {"q_pos": [1e-4, 1e-4, 20.0], "mass": 0.9, "max_thrust": 18.0}],
+    # PIDController's kp / kd aliases (config.get("kp_pos", config.get("kp", ...))) and a common integral limit
+    "pid": [{"kp": [0.02, 0.02, 5.0], "kd": [0.1, 0.1, 2.5], "integral_limit": 2.0},
+            {"kp": [0.01, 0.01, 3.0], "kd_pos": [0.05, 0.05, 1.5], "kd": [9.0, 9.0, 9.0], "integral_limit": 2.0}],
+    "lqr": [{"q_pos": [3e-4, 3e-4, 12.0], "mass": 1.1}, {"r_thrust": 2.0, "mass": 1.0, "max_rate": 2.5}],
+}
+
+
+@pytest.mark.parametrize("kind", ["riccati_lqr", "pid", "lqr"])
+def test_tuner_candidate_keys_reach_the_controller(qt, kind):
+    """Every key of a candidate config reaches its controller, as the
+    reference builds one controller from each whole candidate dict
+    (controllers/tuning.py:832-844): per-candidate mass, PID's kp / kd aliases,
+    common clamps; _evaluate_config's score equals the oracle's for that config."""
+    from quadtrack import tuning
+
+    cands = CAND_EXTRA[kind]
+    if kind == "lqr":  # max_rate only on the second candidate: differs -> must raise
+        cfg = tuning.TuningConfig(controller_type=kind, max_iterations=2, evaluation_episodes=2,
+                                  target_motion_type="circular", episode_length=3.0, evaluation_horizon=300, seed=7)
+        with pytest.raises(ValueError, match="max_rate"):
+            tuning.BatchedTuner(cfg).evaluate_configs(cands)
+        cands = [dict(c, max_rate=2.5) for c in cands]
+    cfg = tuning.TuningConfig(controller_type=kind, max_iterations=2, evaluation_episodes=2,
+                              target_motion_type="circular", episode_length=3.0, evaluation_horizon=300, seed=7)
+    tuner = tuning.BatchedTuner(cfg)
+    batch = tuner.evaluate_configs(cands)
+    env = O.env_params({"simulation": {"max_episode_time": 3.0}, "target": {"motion_type": "circular"}})
+    crit = O.criteria(0.8, 3.0, 0.5)
+    seeds = 7 + np.arange(2)
+    pat, off = O.draws("circular", seeds)
+    x0 = np.array([O.initial_state(env, 2, pat[i], off[i]) for i in range(2)])
+    for k, cand in enumerate(cands):
+        c, K, kc, _, _ = O.controller(dict(cand, controller=kind, dt=0.01) if kind != "riccati_lqr"
+                                      else dict(cand, dt=0.01))
+        met, _, _, _ = O.rollout(env, c, crit, None, pat, None, None, K, kc, False, x0, max_steps=300)
+        ratio = met[:, O.MET_FIELDS.index("on_target_ratio")]
+        err = met[:, O.MET_FIELDS.index("mean_tracking_error")]
+        score = np.mean(list(ratio)) - 0.1 * np.mean(list(err))
+        one, _ = tuner._evaluate_config(cand)
+        assert batch[k][0] == pytest.approx(score, rel=1e-9, abs=1e-9), (k, cand)
+        assert one == pytest.approx(score, rel=1e-9, abs=1e-9), (k, cand)
