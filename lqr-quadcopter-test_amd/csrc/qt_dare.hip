@@ -273,346 +273,583 @@ __global__ __launch_bounds__(256) void dare_axis_kernel(int64_t m, double dt, do
   }
 }
 
-// ----------------------------------------------------------- dense kernel
-
-constexpr int kDenseThreads = 64;
-
-// In-LDS helpers for one wavefront.  Matrices are row-major n x n (ld = n).
-__device__ __forceinline__ void mm(int n, int k, int mcols, const double* a, const double* b, double* c, bool transA = false) {
-  for (int idx = threadIdx.x; idx < n * mcols; idx += kDenseThreads) {
-    const int i = idx / mcols, j = idx % mcols;
-    double s = 0.0;
-    for (int l = 0; l < k; ++l) s += (transA ? a[l * n + i] : a[i * k + l]) * b[l * mcols + j];
-    c[idx] = s;
-  }
-  __syncthreads();
-}
-
-// Gauss-Jordan: W (n x n) is reduced in place, Y (n x ny) receives W^-1 Y.
-__device__ __forceinline__ bool gauss_jordan(int n, double* W, double* Y, int ny, int* piv_sh) {
-  for (int k = 0; k < n; ++k) {
-    if (threadIdx.x == 0) {
-      int p = k;
-      double best = fabs(W[k * n + k]);
-      for (int i = k + 1; i < n; ++i)
-        if (fabs(W[i * n + k]) > best) best = fabs(W[i * n + k]), p = i;
-      piv_sh[0] = best == 0.0 ? -1 : p;
-    }
-    __syncthreads();
-    const int p = piv_sh[0];
-    if (p < 0) return false;
-    if (p != k) {
-      for (int j = threadIdx.x; j < n + ny; j += kDenseThreads) {
-        double* r1 = j < n ? &W[k * n + j] : &Y[k * ny + j - n];
-        double* r2 = j < n ? &W[p * n + j] : &Y[p * ny + j - n];
-        double t = *r1;
-        *r1 = *r2;
-        *r2 = t;
-      }
-    }
-    __syncthreads();
-    const double inv = 1.0 / W[k * n + k];
-    __syncthreads();
-    for (int j = threadIdx.x; j < n + ny; j += kDenseThreads) {
-      if (j < n)
-        W[k * n + j] *= inv;
-      else
-        Y[k * ny + j - n] *= inv;
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < n * (n + ny); idx += kDenseThreads) {
-      const int i = idx / (n + ny), j = idx % (n + ny);
-      if (i == k) continue;
-      const double f = W[i * n + k];
-      if (j < n) {
-        if (j != k) W[i * n + j] -= f * W[k * n + j];
-      } else {
-        Y[i * ny + j - n] -= f * Y[k * ny + j - n];
-      }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += kDenseThreads)
-      if (i != k) W[i * n + k] = 0.0;
-    __syncthreads();
-  }
-  return true;
-}
-
-// eigenvalues of a small symmetric matrix by cyclic Jacobi (one thread)
-__device__ void jacobi_eigs(int n, double* a, double* ev) {
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0.0;
-    for (int i = 0; i < n; ++i)
-      for (int j = i + 1; j < n; ++j) off += a[i * n + j] * a[i * n + j];
-    if (off < 1e-300) break;
-    for (int p = 0; p < n; ++p)
-      for (int q = p + 1; q < n; ++q) {
-        const double apq = a[p * n + q];
-        if (apq == 0.0) continue;
-        const double app = a[p * n + p], aqq = a[q * n + q];
-        const double theta = (aqq - app) / (2.0 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-        for (int k = 0; k < n; ++k) {
-          const double akp = a[k * n + p], akq = a[k * n + q];
-          a[k * n + p] = c * akp - s * akq;
-          a[k * n + q] = s * akp + c * akq;
-        }
-        for (int k = 0; k < n; ++k) {
-          const double apk = a[p * n + k], aqk = a[q * n + k];
-          a[p * n + k] = c * apk - s * aqk;
-          a[q * n + k] = s * apk + c * aqk;
-        }
-      }
-  }
-  for (int i = 0; i < n; ++i) ev[i] = a[i * n + i];
-}
-
-// np.allclose(M, M.T, atol=1e-8) and the eigenvalue test (riccati_lqr.py:70-84, 100-116)
-__device__ bool check_sym_eigs(int n, const double* M, double* scratch, bool strict) {
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      const double a = M[i * n + j], b = M[j * n + i];
-      if (!(fabs(a - b) <= 1e-8 + 1e-5 * fabs(b))) return false;
-    }
-  for (int i = 0; i < n * n; ++i) scratch[i] = M[i];
-  double ev[16];
-  jacobi_eigs(n, scratch, ev);
-  for (int i = 0; i < n; ++i) {
-    if (strict ? !(ev[i] > 1e-10) : (ev[i] < -1e-10)) return false;
-  }
-  return true;
-}
-
 constexpr int kMaxN = 16, kMaxP = 8;
 
-// Dynamic LDS layout of dare_dense_kernel (doubles): sA, sA0, sG, sH, sT2,
-// sQ (n x n); sW (n x n | p x p systems); sY (n x 2n | p x n right-hand
-// sides); sT (n x n | p x n products | the p x p eigen scratch); sB (n x p);
-// sR (p x p).
-struct DenseLds {
-  int nn, w, y, t;
-  __host__ __device__ DenseLds(int n, int p) {
-    nn = n * n;
-    w = nn > p * p ? nn : p * p;
-    y = 2 * nn > p * n ? 2 * nn : p * n;
-    t = nn > p * n ? nn : p * n;
-    t = t > p * p ? t : p * p;
+#ifndef QT_DARE_ROWS_IN_FLIGHT
+#define QT_DARE_ROWS_IN_FLIGHT 3  // rows of a product's right factor loaded ahead of their use
+#endif
+#ifndef QT_DARE_WAVES
+#define QT_DARE_WAVES 2  // minimum waves per SIMD the register allocation must allow
+#endif
+
+// ----------------------------------------------------------- dense kernel
+//
+// General dense SDA for n <= 16 states, p <= 8 inputs: a group of GS lanes
+// per problem (GS = 8 for n <= 6, else 16; one DPP row or half row), 64 / GS
+// problems per wavefront, lane r holding row r of every n x n matrix in
+// registers.  A product X Y reads X from the lane's own row and Y's rows from
+// LDS (the group's lanes read the same addresses: broadcasts); the
+// Gauss-Jordan solves broadcast the pivot row through LDS; reductions
+// (pivot search, norms) are DPP butterflies inside the group.  Every group
+// lives in one wavefront, so its LDS hand-offs need only wave-level ordering
+// (wave_sync): no workgroup barrier, no single-lane serial sections.
+// Sizes are compile-time (N, PP): 6 / 4 (hover LQR), 9 / 4 (hover LQI) and
+// 16 / 8 (anything else), the runtime n x n / p x p problem zero-padded to
+// them — padded rows and columns of A, B, Q, G, H are zero and R's padding is
+// the identity, which decouples them exactly (every padded term is an exact
+// +0 in each sum, pivots stay inside the real block).
+
+// Wave-level ordering of LDS accesses: a wavefront's LDS operations complete
+// in issue order, so a compiler barrier is all a hand-off inside one
+// wavefront needs.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("" ::: "memory");
+}
+
+// A compiler-only memory barrier between two passes over the same LDS rows:
+// without it the loads of the second pass are merged with the first's and
+// every loaded row stays live in registers in between.
+__device__ __forceinline__ void pass_break() { asm volatile("" ::: "memory"); }
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// DPP controls: quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror, row_mirror
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+// Butterfly over a group (GS = 8: a half row, 16: a row); every lane of the
+// group ends with the same value (each step combines commutatively).
+template <int GS, typename Op>
+__device__ __forceinline__ double group_reduce(double v, Op op) {
+  v = op(v, dpp_f64<kDppXor1>(v));
+  v = op(v, dpp_f64<kDppXor2>(v));
+  v = op(v, dpp_f64<kDppHalfMirror>(v));
+  if (GS == 16) v = op(v, dpp_f64<kDppMirror>(v));
+  return v;
+}
+
+template <int GS>
+__device__ __forceinline__ double group_sum(double v) {
+  return group_reduce<GS>(v, [](double a, double b) { return a + b; });
+}
+
+template <int GS>
+__device__ __forceinline__ double group_max(double v) {
+  return group_reduce<GS>(v, [](double a, double b) { return fmax(a, b); });
+}
+
+// This lane's group's bits of a wave ballot, at bit 0.
+template <int GS>
+__device__ __forceinline__ unsigned group_bits(uint64_t ballot) {
+  const int base = (threadIdx.x & 63) & ~(GS - 1);
+  return (unsigned)((ballot >> base) & ((1ull << GS) - 1));
+}
+
+template <int GS>
+__device__ __forceinline__ bool group_all(bool v) {
+  return group_bits<GS>(__ballot(!v)) == 0;
+}
+
+// In-LDS row-major matrix with row stride S (even: rows 16-byte aligned).
+template <int S>
+__device__ __forceinline__ double2 ld2(const double* m, int row, int col2) {
+  return *reinterpret_cast<const double2*>(m + row * S + col2);
+}
+
+// Store this lane's row (NCOL entries) as row `row` of an LDS matrix.
+template <int NCOL, int S>
+__device__ __forceinline__ void st_row(double* m, int row, const double* v) {
+#pragma unroll
+  for (int j = 0; j + 1 < NCOL; j += 2) *reinterpret_cast<double2*>(m + row * S + j) = make_double2(v[j], v[j + 1]);
+  if (NCOL & 1) m[row * S + NCOL - 1] = v[NCOL - 1];
+}
+
+// out[j] = sum_l x[l] Y[l][j] for j < NCOL: this lane's row x (K entries) times
+// the LDS matrix Y (K x NCOL), in the order of the sum index.
+template <int K, int NCOL, int S>
+__device__ __forceinline__ void row_times(const double* x, const double* Y, double* out) {
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) out[j] = 0.0;
+#pragma unroll
+  for (int l = 0; l < K; ++l) {
+#pragma unroll
+    for (int j = 0; j + 1 < NCOL; j += 2) {
+      const double2 y = ld2<S>(Y, l, j);
+      out[j] += x[l] * y.x;
+      out[j + 1] += x[l] * y.y;
+    }
+    if (NCOL & 1) out[NCOL - 1] += x[l] * Y[l * S + NCOL - 1];
+    // keep the scheduler from hoisting every row's loads to the top (it would
+    // hold all K rows in registers and halve the waves per SIMD)
+    if ((l % QT_DARE_ROWS_IN_FLIGHT) == QT_DARE_ROWS_IN_FLIGHT - 1) __builtin_amdgcn_sched_barrier(0);
   }
-  __host__ __device__ int doubles(int n, int p) const { return 6 * nn + w + y + t + n * p + p * p; }
+}
+
+// Gauss-Jordan with partial pivoting on the group's NR x NC augmented system,
+// row r of it in this lane's w (lanes r >= NR hold no row).  Rows are not
+// swapped: the row chosen for pivot column k stays in its lane, which records
+// k in *col.  The pivot row is normalised (multiplied by the reciprocal of
+// its pivot) and broadcast through `piv` (LDS, NC doubles); every other row
+// subtracts its multiple.  Ties take the lowest row.  Returns false (uniform
+// over the group) when a pivot column is all zero.
+template <int NR, int NC, int GS>
+__device__ __forceinline__ bool group_gauss_jordan(double (&w)[NC], int r, double* piv, int* col) {
+  bool used = r >= NR;
+  *col = -1;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const double cand = used ? -1.0 : fabs(w[k]);
+    const double mx = group_max<GS>(cand);
+    if (!(mx > 0.0)) return false;
+    const int p = __builtin_ctz(group_bits<GS>(__ballot(!used && cand == mx)));
+    if (r == p) {
+      const double inv = 1.0 / w[k];
+#pragma unroll
+      for (int j = k; j < NC; ++j) w[j] *= inv;
+      // columns < k of a pivot row are already zero: only k+1.. go out
+#pragma unroll
+      for (int j = (k + 1) & ~1; j + 1 < NC; j += 2) *reinterpret_cast<double2*>(piv + j) = make_double2(w[j], w[j + 1]);
+      if (NC & 1) piv[NC - 1] = w[NC - 1];
+      used = true;
+      *col = k;
+    }
+    wave_sync();
+    if (r != p) {  // lanes r >= NR eliminate too: their values are never used
+      const double f = w[k];
+#pragma unroll
+      for (int j = (k + 1) & ~1; j + 1 < NC; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(piv + j);
+        if (j > k) w[j] -= f * v.x;
+        w[j + 1] -= f * v.y;
+      }
+      if (NC & 1) w[NC - 1] -= f * piv[NC - 1];
+      w[k] = 0.0;
+    }
+    wave_sync();
+  }
+  return true;
+}
+
+// In-place Gauss-Jordan inversion with partial pivoting of the group's
+// NR x NR matrix W, row r in this lane's w (lanes r >= NR hold no row).  Rows
+// are not swapped: pk[k] records the lane whose row became pivot k (the same
+// in every lane of the group) and *col the pivot this lane's row became.
+// Each step broadcasts the NR-entry pivot row through `piv` (LDS).  On return
+// the lanes hold S with  W^-1[a][pk[k]] = S[pk[a]][k],  so row a of W^-1 X is
+// sum_k S[pk[a]][k] X[pk[k]][:], which lane pk[a] (*col = a) forms by reading
+// X's rows in pk order.  Ties take the lowest row.  Returns false (uniform over
+// the group) when a pivot column is all zero.
+template <int NR, int GS>
+__device__ __forceinline__ bool group_gj_invert(double (&w)[NR], int r, double* piv, int (&pk)[NR], int* col) {
+  bool used = r >= NR;
+  *col = -1;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const double cand = used ? -1.0 : fabs(w[k]);
+    const double mx = group_max<GS>(cand);
+    if (!(mx > 0.0)) return false;
+    const int p = __builtin_ctz(group_bits<GS>(__ballot(!used && cand == mx)));
+    pk[k] = p;
+    if (r == p) {
+      const double inv = 1.0 / w[k];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) w[j] = j == k ? inv : w[j] * inv;
+      st_row<NR, NR + (NR & 1)>(piv, 0, w);
+      used = true;
+      *col = k;
+    }
+    wave_sync();
+    if (r != p) {  // lanes r >= NR eliminate too: their values are never used
+      const double f = w[k];
+#pragma unroll
+      for (int j = 0; j + 1 < NR; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(piv + j);
+        w[j] = j == k ? -f * v.x : w[j] - f * v.x;
+        w[j + 1] = j + 1 == k ? -f * v.y : w[j + 1] - f * v.y;
+      }
+      if (NR & 1) w[NR - 1] = NR - 1 == k ? -f * piv[NR - 1] : w[NR - 1] - f * piv[NR - 1];
+    }
+    wave_sync();
+  }
+  return true;
+}
+
+// Row-per-lane Cholesky test of the group's N x N matrix c (row r in this
+// lane): true iff every pivot is > 0, i.e. c is positive definite.  The
+// column of each step goes through `colbuf` (LDS, N doubles).
+template <int N, int GS>
+__device__ __forceinline__ bool group_cholesky_pd(double (&c)[N], int r, double* colbuf) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (r < N) colbuf[r] = c[k];
+    wave_sync();
+    const double d = colbuf[k];
+    ok = ok && d > 0.0;
+    const double isd = 1.0 / sqrt(d);  // a definiteness test: the reciprocal's rounding is immaterial
+    const double lr = c[k] * isd;
+#pragma unroll
+    for (int j = k + 1; j < N; ++j) c[j] -= lr * (colbuf[j] * isd);
+    wave_sync();
+  }
+  return ok;
+}
+
+// np.allclose(M, M.T, atol=1e-8) (riccati_lqr.py:70-84, 100-116) for the
+// group's N x N matrix, row r in this lane, via `buf` (LDS, N x S).
+template <int N, int S, int GS>
+__device__ __forceinline__ bool group_symmetric(const double (&row)[N], int r, double* buf) {
+  if (r < N) st_row<N, S>(buf, r, row);
+  wave_sync();
+  bool ok = true;
+  if (r < N) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double b = buf[j * S + r];
+      ok = ok && fabs(row[j] - b) <= 1e-8 + 1e-5 * fabs(b);
+    }
+  }
+  wave_sync();
+  return group_all<GS>(ok);
+}
+
+template <int N, int PP, int GS>
+struct GroupDims {
+  static constexpr int kProblemsPerWave = 64 / GS;
+  static constexpr int S = (N + 1) & ~1;                   // LDS row stride (doubles)
+  static constexpr int MAT = N * S;
+  static constexpr int RAW = 5 * MAT;                       // H, A, Y1, T (also the pivot / column buffer), G
+  // per-problem stride = 8 (mod 32) doubles: the 64 / GS problems of a wave
+  // start 16 banks apart, so their broadcast reads do not conflict
+  static constexpr int PROB = RAW + ((8 - RAW % 32) + 32) % 32;
+  static_assert(3 * N <= MAT && PP + N <= MAT && N <= GS && PP <= GS, "group layout");
 };
 
-inline size_t dense_lds_bytes(int n, int p) { return sizeof(double) * (size_t)DenseLds(n, p).doubles(n, p); }
 
-// General dense SDA, one wavefront per problem.  Hover model (A, B == NULL):
-// A, B built from (dt, mass, gravity) exactly as build_linearized_system /
-// build_augmented_lqi_system; otherwise A [n*n] and B [n*p] are read (shared
-// when ab_per_problem == 0).  With `fallback`, invalid or failed hover-model
-// problems get the heuristic gains (riccati_lqr.py:747-777).
-// NT, PT: compile-time n, p (the 6-state hover model, 4 inputs): the LDS
-// index arithmetic (idx / n, idx % n) becomes multiplications and the short
-// loops unroll (2.5 -> 2.2 ms per 65,536 problems); 0 = sizes at run time.
-template <int NT, int PT>
-__global__ __launch_bounds__(kDenseThreads) void dare_dense_kernel(int n_rt, int p_rt, int64_t m,
-                                                                   const double* __restrict__ Ain,
-                                                                   const double* __restrict__ Bin,
-                                                                   int ab_per_problem, double dt, double gravity,
-                                                                   const double* __restrict__ mass,
-                                                                   const double* __restrict__ q,
-                                                                   const double* __restrict__ r, int fallback,
-                                                                   double* K, double* P, int8_t* status,
-                                                                   int32_t* iters) {
-  const int n = NT ? NT : n_rt, p = PT ? PT : p_rt;
-  const int64_t pb = blockIdx.x;
-  if (pb >= m) return;
-  // LDS sized to the problem (dense_lds_bytes): ~7 KB at n = 9, p = 4, so
-  // ~20 problems share a CU instead of the 6 that fixed 16 x 16 arrays allowed
-  extern __shared__ double smem[];
-  const DenseLds L(n, p);
-  double* sA = smem;
-  double* sA0 = sA + L.nn;
-  double* sB = sA0 + L.nn;
-  double* sG = sB + n * p;
-  double* sH = sG + L.nn;
-  double* sW = sH + L.nn;
-  double* sY = sW + L.w;
-  double* sT = sY + L.y;
-  double* sT2 = sT + L.t;
-  double* sR = sT2 + L.nn;
-  double* sQ = sR + p * p;
-  __shared__ int sh_i[2];
-  const int tid = threadIdx.x;
+template <int N, int PP, int GS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVES, 8))) void dare_group_kernel(int n, int p, int64_t m, const double* __restrict__ Ain,
+                                                        const double* __restrict__ Bin, int ab_per_problem,
+                                                        double dt, double gravity, const double* __restrict__ mass,
+                                                        const double* __restrict__ q, const double* __restrict__ rin,
+                                                        int fallback, double* K, double* P, int8_t* status,
+                                                        int32_t* iters) {
+  using D = GroupDims<N, PP, GS>;
+  constexpr int S = D::S, MAT = D::MAT, NC = 3 * N;
+  __shared__ __attribute__((aligned(16))) double lds[D::kProblemsPerWave * D::PROB];
+  const int lane = threadIdx.x & 63, g = lane / GS, r = lane % GS;
+  // rows read by lanes past the matrix (r >= N, r >= PP): a real row, so the
+  // loads need no branch; such lanes' values are never stored, never pivot
+  // and are zeroed before every group reduction
+  const int rc = r < N ? r : N - 1, rp = r < PP ? r : PP - 1;
+  const int64_t pb = (int64_t)blockIdx.x * D::kProblemsPerWave + g;
+  const bool valid = pb < m;  // uniform over the group
+  double* Hl = lds + g * D::PROB;
+  double* Al = Hl + MAT;
+  double* Yl = Al + MAT;
+  double* Tl = Yl + MAT;
+  double* Gl = Tl + MAT;
   const bool hover = Ain == nullptr;
-  const double mss = mass ? mass[pb] : 1.0;
+  const double mss = (valid && mass) ? mass[pb] : 1.0;
   const int64_t abm = ab_per_problem ? m : 1, abj = ab_per_problem ? pb : 0;
-  for (int i = tid; i < n * n; i += kDenseThreads) {
-    sQ[i] = q[(int64_t)i * m + pb];
-    double v;
-    if (hover) {
-      const int a = i / n, b = i % n;
-      v = (a == b) ? 1.0 : 0.0;
-      if (a < 3 && b == a + 3) v = dt;             // A_d = I + A_c dt (riccati_lqr.py:260)
-      if (n == 9 && a >= 6 && b == a - 6) v = dt;  // integral rows (308)
-    } else {
-      v = Ain[(int64_t)i * abm + abj];
-    }
-    sA[i] = v;
-    sA0[i] = v;
+  const bool real = valid && r < n;
+
+  // ---- inputs, read where they are used (the doubling loop keeps only G in
+  // registers across its solve): A, B (N-row padded), R (PP-row padded)
+  auto a_in = [&](int j) -> double {
+    if (!(real && j < n)) return 0.0;
+    if (!hover) return Ain[(int64_t)(r * n + j) * abm + abj];
+    double a = (r == j) ? 1.0 : 0.0;
+    if (r < 3 && j == r + 3) a = dt;             // A_d = I + A_c dt (riccati_lqr.py:260)
+    if (n == 9 && r >= 6 && j == r - 6) a = dt;  // integral rows (308)
+    return a;
+  };
+  auto b_in = [&](int c) -> double {
+    if (!(real && c < p)) return 0.0;
+    if (!hover) return Bin[(int64_t)(r * p + c) * abm + abj];
+    if (r == 5 && c == 0) return 1.0 / mss * dt;  // riccati_lqr.py:250,261
+    if (r == 4 && c == 1) return -gravity * dt;   // 252
+    if (r == 3 && c == 2) return gravity * dt;    // 254
+    return 0.0;
+  };
+  auto r_in = [&](int c) -> double {
+    return (valid && r < p && c < p) ? rin[(int64_t)(r * p + c) * m + pb] : (r == c ? 1.0 : 0.0);
+  };
+
+  // ---- validation (_is_positive_semidefinite / _is_positive_definite,
+  // riccati_lqr.py:57-116): symmetric within np.allclose, then the
+  // eigenvalue bounds as Cholesky tests: min eig(Q) >= -1e-10 <=> Q + 1e-10 I
+  // positive definite, min eig(R) > 1e-10 <=> R - 1e-10 I positive definite
+  // (the same decisions but on the boundary itself, to rounding)
+  double Hr[N];  // H = Q to start
+#pragma unroll
+  for (int j = 0; j < N; ++j) Hr[j] = (real && j < n) ? q[(int64_t)(r * n + j) * m + pb] : 0.0;
+  int st = QT_DARE_OK;
+  {
+    bool qok = group_symmetric<N, S, GS>(Hr, r, Tl);
+    double c[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) c[j] = Hr[j] + ((r == j) ? 1e-10 : 0.0);
+    qok = group_cholesky_pd<N, GS>(c, r, Tl) && qok;
+    double rr[PP];
+#pragma unroll
+    for (int j = 0; j < PP; ++j) rr[j] = r_in(j);
+    bool rok = group_symmetric<PP, S, GS>(rr, r, Tl);
+#pragma unroll
+    for (int j = 0; j < PP; ++j) rr[j] -= (r == j) ? 1e-10 : 0.0;
+    rok = group_cholesky_pd<PP, GS>(rr, r, Tl) && rok;
+    st = !qok ? QT_DARE_Q_NOT_PSD : (!rok ? QT_DARE_R_NOT_PD : QT_DARE_OK);
   }
-  for (int i = tid; i < p * p; i += kDenseThreads) sR[i] = r[(int64_t)i * m + pb];
-  for (int i = tid; i < n * p; i += kDenseThreads) {
-    double v = 0.0;
-    if (hover) {
-      const int a = i / p, c = i % p;
-      if (a == 5 && c == 0) v = 1.0 / mss * dt;  // riccati_lqr.py:250,261
-      if (a == 4 && c == 1) v = -gravity * dt;   // 252
-      if (a == 3 && c == 2) v = gravity * dt;    // 254
-    } else {
-      v = Bin[(int64_t)i * abm + abj];
-    }
-    sB[i] = v;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int st = QT_DARE_OK;
-    if (!check_sym_eigs(n, sQ, sT, false))
-      st = QT_DARE_Q_NOT_PSD;
-    else if (!check_sym_eigs(p, sR, sT, true))
-      st = QT_DARE_R_NOT_PD;
-    sh_i[1] = st;
-  }
-  __syncthreads();
-  int st = sh_i[1];
+
+  // ---- G = B R^-1 B': X = R^-1 B' by Gauss-Jordan on [R | B'] (lanes r < PP), G = B X
+  double Gr[N];
   int it = 0;
-  if (st == QT_DARE_OK) {
-    // G = B R^-1 B' : solve R X = B' (p x n), then G = B X
-    for (int i = tid; i < p * p; i += kDenseThreads) sW[i] = sR[i];
-    for (int i = tid; i < p * n; i += kDenseThreads) sY[i] = sB[(i % n) * p + i / n];
-    __syncthreads();
-    if (!gauss_jordan(p, sW, sY, n, sh_i)) st = QT_DARE_SINGULAR;
-    if (st == QT_DARE_OK) {
-      mm(n, p, n, sB, sY, sG);
-      for (int i = tid; i < n * n; i += kDenseThreads) sH[i] = sQ[i];
-      __syncthreads();
-      bool conv = false;
-      for (it = 1; it <= kMaxIter; ++it) {
-        mm(n, n, n, sG, sH, sW);
-        for (int i = tid; i < n; i += kDenseThreads) sW[i * n + i] += 1.0;
-        for (int i = tid; i < n * n; i += kDenseThreads) {
-          const int a = i / n, b = i % n;
-          sY[a * 2 * n + b] = sA[i];
-          sY[a * 2 * n + n + b] = sG[i];
-        }
-        __syncthreads();
-        if (!gauss_jordan(n, sW, sY, 2 * n, sh_i)) {
-          st = QT_DARE_SINGULAR;
-          break;
-        }
-        // Y1 = sY[:, :n], Y2 = sY[:, n:] (ld 2n).  T = H Y1 ; T2 = A' T
-        for (int idx = tid; idx < n * n; idx += kDenseThreads) {
-          const int i = idx / n, j = idx % n;
-          double s = 0.0;
-          for (int l = 0; l < n; ++l) s += sH[i * n + l] * sY[l * 2 * n + j];
-          sT[idx] = s;
-        }
-        __syncthreads();
-        mm(n, n, n, sA, sT, sT2, true);
-        for (int idx = tid; idx < n * n; idx += kDenseThreads) {
-          const int i = idx / n, j = idx % n;
-          sW[idx] = sH[idx] + 0.5 * (sT2[i * n + j] + sT2[j * n + i]);
-        }
-        __syncthreads();
-        if (tid == 0) {
-          double dn = 0.0, hn = 0.0;
-          for (int i = 0; i < n * n; ++i) {
-            dn += (sW[i] - sH[i]) * (sW[i] - sH[i]);
-            hn += sW[i] * sW[i];
-          }
-          sh_i[0] = !isfinite(hn) ? -1 : (sqrt(dn) <= kTol * sqrt(hn) ? 1 : 0);
-        }
-        __syncthreads();
-        const int flag = sh_i[0];
-        for (int i = tid; i < n * n; i += kDenseThreads) sH[i] = sW[i];
-        // T = Y2 A' ; T2 = A T ; G += sym(T2)
-        for (int idx = tid; idx < n * n; idx += kDenseThreads) {
-          const int i = idx / n, j = idx % n;
-          double s = 0.0;
-          for (int l = 0; l < n; ++l) s += sY[i * 2 * n + n + l] * sA[j * n + l];
-          sT[idx] = s;
-        }
-        __syncthreads();
-        mm(n, n, n, sA, sT, sT2);
-        for (int idx = tid; idx < n * n; idx += kDenseThreads) {
-          const int i = idx / n, j = idx % n;
-          sG[idx] += 0.5 * (sT2[i * n + j] + sT2[j * n + i]);
-        }
-        // A = A Y1
-        for (int idx = tid; idx < n * n; idx += kDenseThreads) {
-          const int i = idx / n, j = idx % n;
-          double s = 0.0;
-          for (int l = 0; l < n; ++l) s += sA[i * n + l] * sY[l * 2 * n + j];
-          sT[idx] = s;
-        }
-        __syncthreads();
-        for (int i = tid; i < n * n; i += kDenseThreads) sA[i] = sT[i];
-        __syncthreads();
-        if (flag < 0) {
-          st = QT_DARE_NO_CONVERGE;
-          break;
-        }
-        if (flag == 1) {
-          conv = true;
-          break;
-        }
+  bool conv = false;
+  {
+    double br[PP];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) br[c] = b_in(c);
+    if (r < N) st_row<PP, S>(Yl, r, br);  // B (N x PP) for its columns
+    wave_sync();
+    double w[PP + N];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) w[c] = r_in(c);
+#pragma unroll
+    for (int j = 0; j < N; ++j) w[PP + j] = r < PP ? Yl[j * S + rp] : 0.0;
+    wave_sync();
+    int col;
+    const bool ok = group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col);
+    if (st == QT_DARE_OK && !ok) st = QT_DARE_SINGULAR;
+    if (col >= 0) st_row<N, S>(Yl, col, w + PP);  // X row `col`
+    wave_sync();
+    row_times<PP, N, S>(br, Yl, Gr);
+    wave_sync();
+  }
+  if (r < N) {
+    double ar[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) ar[j] = a_in(j);
+    st_row<N, S>(Hl, r, Hr);
+    st_row<N, S>(Al, r, ar);
+  }
+  wave_sync();
+
+  // ---- doublings (the SDA iteration of dare_axis_kernel / riccati_lqr.py's
+  // fixed point): W = I + G H ; [Y1 Y2] = W^-1 [A G] ; H += sym(A' H Y1) ;
+  // G += sym(A Y2 A') ; A = A Y1, until |dH|_F <= tol |H|_F.  H, A and G's
+  // copy live in LDS (Hl, Al, Gl); W^-1 comes from an in-place inversion
+  // (N-entry pivot rows) and is applied to A and G as products; every
+  // intermediate product goes back to LDS at once (short register lifetimes).
+  if (r < N) st_row<N, S>(Gl, r, Gr);
+  wave_sync();
+  while (true) {
+    const bool act = valid && st == QT_DARE_OK && !conv && it < kMaxIter;  // uniform over the group
+    if (__ballot(act) == 0) break;
+    if (!act) continue;
+    ++it;
+    int col, pk[N];
+    {
+      double w[N];
+      row_times<N, N, S>(Gr, Hl, w);  // W = G H, then + I
+#pragma unroll
+      for (int j = 0; j < N; ++j) w[j] = j == r ? w[j] + 1.0 : w[j];
+      if (!group_gj_invert<N, GS>(w, r, Tl, pk, &col)) {
+        st = QT_DARE_SINGULAR;
+        continue;
       }
-      if (st == QT_DARE_OK && !conv) st = QT_DARE_NO_CONVERGE;
+      // Y1, Y2 rows `col`: sum_k S[k] A[pk[k]], sum_k S[k] G[pk[k]]
+      double y1[N], y2[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) y1[j] = 0.0, y2[j] = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const double* ar = Al + pk[k] * S;
+        const double* gp = Gl + pk[k] * S;
+#pragma unroll
+        for (int j = 0; j + 1 < N; j += 2) {
+          const double2 a = *reinterpret_cast<const double2*>(ar + j);
+          const double2 gg = *reinterpret_cast<const double2*>(gp + j);
+          y1[j] += w[k] * a.x, y1[j + 1] += w[k] * a.y;
+          y2[j] += w[k] * gg.x, y2[j + 1] += w[k] * gg.y;
+        }
+        if (N & 1) y1[N - 1] += w[k] * ar[N - 1], y2[N - 1] += w[k] * gp[N - 1];
+      }
+      if (col >= 0) {
+        st_row<N, S>(Yl, col, y1);
+        st_row<N, S>(Tl, col, y2);
+      }
+    }
+    wave_sync();
+    double y2[N], t[N], hr[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) y2[j] = Tl[rc * S + j], hr[j] = Hl[rc * S + j];
+    // T = H Y1 ; M = A' T ; H' = H + (M + M') / 2
+    row_times<N, N, S>(hr, Yl, t);
+    wave_sync();
+    if (r < N) st_row<N, S>(Tl, r, t);
+    wave_sync();
+    {
+      double ac[N];  // column r of A
+#pragma unroll
+      for (int l = 0; l < N; ++l) ac[l] = Al[l * S + rc];
+      row_times<N, N, S>(ac, Tl, t);
+    }
+    wave_sync();
+    if (r < N) st_row<N, S>(Tl, r, t);
+    wave_sync();
+    double dn = 0.0, hn = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double hnew = hr[j] + 0.5 * (t[j] + Tl[j * S + rc]);
+      dn += (hnew - hr[j]) * (hnew - hr[j]);
+      hn += hnew * hnew;
+      hr[j] = hnew;
+    }
+    dn = group_sum<GS>(r < N ? dn : 0.0);
+    hn = group_sum<GS>(r < N ? hn : 0.0);
+    const int flag = !isfinite(hn) ? -1 : (sqrt(dn) <= kTol * sqrt(hn) ? 1 : 0);
+    wave_sync();
+    if (r < N) st_row<N, S>(Hl, r, hr);
+    // T = Y2 A' ; M = A T ; G' = G + (M + M') / 2
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int l = 0; l + 1 < N; l += 2) {
+        const double2 a = ld2<S>(Al, j, l);
+        s2 += y2[l] * a.x;
+        s2 += y2[l + 1] * a.y;
+      }
+      if (N & 1) s2 += y2[N - 1] * Al[j * S + N - 1];
+      t[j] = s2;
+    }
+    wave_sync();
+    if (r < N) st_row<N, S>(Tl, r, t);
+    wave_sync();
+    double ar[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) ar[j] = Al[rc * S + j];
+    row_times<N, N, S>(ar, Tl, t);
+    wave_sync();
+    if (r < N) st_row<N, S>(Tl, r, t);
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < N; ++j) Gr[j] += 0.5 * (t[j] + Tl[j * S + rc]);
+    // A = A Y1
+    row_times<N, N, S>(ar, Yl, t);
+    wave_sync();
+    if (r < N) {
+      st_row<N, S>(Al, r, t);
+      st_row<N, S>(Gl, r, Gr);
+    }
+    wave_sync();
+    if (flag < 0) st = QT_DARE_NO_CONVERGE;
+    if (flag == 1) conv = true;
+  }
+  if (valid && st == QT_DARE_OK && !conv) st = QT_DARE_NO_CONVERGE;
+
+  // ---- K = (R + B'PB)^-1 B'PA (riccati_lqr.py:181-182): T = B'P (lanes r < PP),
+  // W = R + T B, Y = T A0, solve W K = Y
+  if (valid && st == QT_DARE_OK) {
+    // B (for its columns and rows) and the original A back to LDS
+    wave_sync();
+    if (r < N) {
+      double br[PP], ar[N];
+#pragma unroll
+      for (int c = 0; c < PP; ++c) br[c] = b_in(c);
+#pragma unroll
+      for (int j = 0; j < N; ++j) ar[j] = a_in(j);
+      st_row<PP, S>(Yl, r, br);
+      st_row<N, S>(Al, r, ar);
+    }
+    wave_sync();
+    double bc[N], tr[N];  // column r of B ; row r of T = B' P
+#pragma unroll
+    for (int l = 0; l < N; ++l) bc[l] = Yl[l * S + rp];
+    row_times<N, N, S>(bc, Hl, tr);
+    double w[PP + N];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) {
+      double s = r_in(c);
+#pragma unroll
+      for (int l = 0; l < N; ++l) s += tr[l] * Yl[l * S + c];
+      w[c] = s;
+    }
+    row_times<N, N, S>(tr, Al, w + PP);
+    wave_sync();
+    int col;
+    if (!group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col)) st = QT_DARE_SINGULAR;
+    if (st == QT_DARE_OK && col >= 0 && col < p) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < n) K[(int64_t)(col * n + j) * m + pb] = w[PP + j];
     }
   }
-  if (st == QT_DARE_OK) {
-    // K = (R + B'PB)^-1 B'PA : T = B'P (p x n), W = R + T B (p x p), Y = T A0 (p x n)
-    mm(p, n, n, sB, sH, sT, true);
-    for (int idx = tid; idx < p * p; idx += kDenseThreads) {
-      const int i = idx / p, j = idx % p;
-      double s = sR[idx];
-      for (int l = 0; l < n; ++l) s += sT[i * n + l] * sB[l * p + j];
-      sW[idx] = s;
+  if (!valid) return;
+  const bool ok = st == QT_DARE_OK;
+  if (ok) {
+    if (P && r < n) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < n) P[(int64_t)(r * n + j) * m + pb] = Hl[r * S + j];
     }
-    for (int idx = tid; idx < p * n; idx += kDenseThreads) {
-      const int i = idx / n, j = idx % n;
-      double s = 0.0;
-      for (int l = 0; l < n; ++l) s += sT[i * n + l] * sA0[l * n + j];
-      sY[idx] = s;
-    }
-    __syncthreads();
-    if (!gauss_jordan(p, sW, sY, n, sh_i)) st = QT_DARE_SINGULAR;
-  }
-  if (st == QT_DARE_OK) {
-    for (int i = tid; i < p * n; i += kDenseThreads) K[(int64_t)i * m + pb] = sY[i];
-    if (P)
-      for (int i = tid; i < n * n; i += kDenseThreads) P[(int64_t)i * m + pb] = sH[i];
   } else {
-    for (int i = tid; i < p * n; i += kDenseThreads) K[(int64_t)i * m + pb] = 0.0;
-    if (P)
-      for (int i = tid; i < n * n; i += kDenseThreads) P[(int64_t)i * m + pb] = 0.0;
-    __syncthreads();
-    if (fallback && hover && tid == 0) {
+    if (r < p) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < n) K[(int64_t)(r * n + j) * m + pb] = 0.0;
+    }
+    if (P && r < n) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < n) P[(int64_t)(r * n + j) * m + pb] = 0.0;
+    }
+  }
+  // one status / fallback per problem (st is uniform over the group), from its first lane
+  if (r == 0) {
+    if (!ok && fallback && hover) {
       // heuristic gains from the diagonals (riccati_lqr.py:756-774)
-      const double rrate = (sR[5] + sR[10] + sR[15]) / 3.0;
+      auto qd = [&](int i) { return q[(int64_t)(i * n + i) * m + pb]; };
+      auto rd = [&](int i) { return rin[(int64_t)(i * p + i) * m + pb]; };
+      const double rrate = (rd(1) + rd(2) + rd(3)) / 3.0;
       double kp, kv;
-      heuristic_axis(sQ[2 * n + 2], sQ[5 * n + 5], sR[0], kp, kv);
+      heuristic_axis(qd(2), qd(5), rd(0), kp, kv);
       K[(int64_t)(0 * n + 2) * m + pb] = kp;
       K[(int64_t)(0 * n + 5) * m + pb] = kv;
-      heuristic_axis(sQ[1 * n + 1], sQ[4 * n + 4], rrate, kp, kv);
+      heuristic_axis(qd(1), qd(4), rrate, kp, kv);
       K[(int64_t)(1 * n + 1) * m + pb] = -kp;
       K[(int64_t)(1 * n + 4) * m + pb] = -kv;
-      heuristic_axis(sQ[0], sQ[3 * n + 3], rrate, kp, kv);
+      heuristic_axis(qd(0), qd(3), rrate, kp, kv);
       K[(int64_t)(2 * n + 0) * m + pb] = kp;
       K[(int64_t)(2 * n + 3) * m + pb] = kv;
     }
-  }
-  if (tid == 0) {
     status[pb] = (int8_t)st;
     if (iters) iters[pb] = it;
+  }
+}
+
+// Launch the group kernel sized for (n, p): 6 / 4, 9 / 4, else 16 / 8.
+inline void launch_dare_group(int n, int p, int64_t m, const double* A, const double* B, int ab_per_problem,
+                              double dt, double gravity, const double* mass, const double* q, const double* r,
+                              int fallback, double* K, double* P, int8_t* status, int32_t* iters, hipStream_t s) {
+  if (n <= 6 && p <= 4) {
+    const int grid = (int)((m + 7) / 8);
+    dare_group_kernel<6, 4, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
+                                                   fallback, K, P, status, iters);
+  } else if (n <= 9 && p <= 4) {
+    const int grid = (int)((m + 3) / 4);
+    dare_group_kernel<9, 4, 16><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
+                                                    fallback, K, P, status, iters);
+  } else {
+    const int grid = (int)((m + 3) / 4);
+    dare_group_kernel<16, 8, 16><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
+                                                     fallback, K, P, status, iters);
   }
 }
 
@@ -633,13 +870,8 @@ extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gra
     else
       dare_axis_kernel<6><<<grid, 256, 0, s>>>(m, dt, gravity, mass, q, r, K, P, status, iters);
   } else {
-    if (m > 0x7fffffff) return QT_EINVAL;
-    if (n_state == 9)  // runtime sizes: the unrolled 9-state form needs 169 VGPRs and ran 1.8x slower
-      dare_dense_kernel<0, 0><<<(int)m, kDenseThreads, dense_lds_bytes(9, 4), s>>>(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r,
-                                                       1, K, P, status, iters);
-    else
-      dare_dense_kernel<6, 4><<<(int)m, kDenseThreads, dense_lds_bytes(6, 4), s>>>(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r,
-                                                       1, K, P, status, iters);
+    if (m > ((int64_t)0x7fffffff) * 4) return QT_EINVAL;
+    launch_dare_group(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r, 1, K, P, status, iters, s);
   }
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }
@@ -647,16 +879,10 @@ extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gra
 extern "C" int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, const double* B,
                              int32_t ab_per_problem, const double* q, const double* r, double* K, double* P,
                              int8_t* status, int32_t* iters, void* stream) {
-  if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > 0x7fffffff) return QT_EINVAL;
+  if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > ((int64_t)0x7fffffff) * 4) return QT_EINVAL;
   if (m == 0) return QT_OK;  // empty: no pointer is read
   if (!A || !B || !q || !r || !K || !status) return QT_EINVAL;
-  hipStream_t hs = (hipStream_t)stream;
-  const size_t lds = dense_lds_bytes(n, p);
-  if (n == 6 && p == 4)
-    dare_dense_kernel<6, 4><<<(int)m, kDenseThreads, lds, hs>>>(n, p, m, A, B, ab_per_problem, 0.0, 0.0,
-                                                                       nullptr, q, r, 0, K, P, status, iters);
-  else
-    dare_dense_kernel<0, 0><<<(int)m, kDenseThreads, lds, hs>>>(n, p, m, A, B, ab_per_problem, 0.0, 0.0,
-                                                                       nullptr, q, r, 0, K, P, status, iters);
+  launch_dare_group(n, p, m, A, B, ab_per_problem, 0.0, 0.0, nullptr, q, r, 0, K, P, status, iters,
+                    (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }

@@ -94,12 +94,40 @@ struct BatchDev {
   const int32_t* order;
   const double* ff;         // [7][n] per-episode feed-forward (qt_batch.ff) or NULL
   int64_t slot0, slot_end;  // the slot range this launch covers (grouped launches)
+  // Wave-aligned motion groups (one-launch grouped rollout): group i covers
+  // slots [seg_end[i-1], seg_end[i]) of motion seg_motion[i] and starts a new
+  // wavefront (waves [wave_end[i-1], wave_end[i])), so every wave holds one
+  // motion type.  nseg = 0: slots follow launch positions (slot0 + p).
+  int32_t nseg;
+  int8_t seg_motion[8];
+  int64_t seg_end[8], wave_end[8];
 };
 
-// The slot a launch position runs, or -1 past the launch's slot range.
+// The slot a launch position runs, or -1 past the launch's slot range (or in
+// the unused tail of a group's last wave).
 __device__ __forceinline__ int64_t slot_at(const BatchDev& b, int64_t p) {
-  const int64_t slot = b.slot0 + p;
-  return slot < b.slot_end ? slot : -1;
+  if (b.nseg == 0) {
+    const int64_t slot = b.slot0 + p;
+    return slot < b.slot_end ? slot : -1;
+  }
+  const int64_t w = p >> 6;
+  int64_t s0 = 0, w0 = 0;
+  for (int i = 0; i < b.nseg; ++i) {  // uniform per wave
+    if (w < b.wave_end[i]) {
+      const int64_t slot = s0 + ((w - w0) << 6) + (p & 63);
+      return slot < b.seg_end[i] ? slot : -1;
+    }
+    s0 = b.seg_end[i], w0 = b.wave_end[i];
+  }
+  return -1;
+}
+
+// The motion of a wave-aligned group's wave (b.nseg > 0), uniform per wave.
+__device__ __forceinline__ int wave_motion(const BatchDev& b, int64_t p) {
+  const int64_t w = p >> 6;
+  for (int i = 0; i < b.nseg; ++i)
+    if (w < b.wave_end[i]) return b.seg_motion[i];
+  return -1;
 }
 
 // The lane's feed-forward parameters: per episode (qt_batch.ff rows: velocity
@@ -713,27 +741,22 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type
 // (qt_rollout_grouped: `order` lists the episodes motion by motion) in ONE
-// launch: each wave runs the loop specialised for its motion; a wave that
-// straddles two groups (at most one per group boundary) runs the
-// runtime-motion loop, whose target arithmetic per lane is the specialised
-// loops' own (rotor_target_rt), so results do not depend on the wave.  One
-// launch keeps every SIMD busy where one launch per group would run each
-// group's waves alone (65,536 episodes of five groups: ~205 waves per launch
-// on 1,024 SIMDs), and wave count stays ceil(n / 64).
+// launch: the groups start at wavefront boundaries (BatchDev's wave-aligned
+// segments), so each wave runs the loop specialised for its motion and no
+// wave needs a runtime-motion loop; the last wave of a group may be partly
+// empty (at most one per group).  One launch keeps every SIMD busy where one
+// launch per group would run each group's waves alone (65,536 episodes of five
+// groups: ~205 waves per launch on 1,024 SIMDs).
 // Two waves per SIMD: mixed batches are large (config 5: 1,048,576 episodes,
 // 16 waves per SIMD on one GPU, 2 on each of 8), and a second resident wave
-// issues in the first one's stall and encoding slots.  The register budget
-// of 256 spills ~58 VGPRs to scratch, and still: 27.7 -> 25.0 ms for config 5
-// on one GPU (occupancy 1: 256 VGPRs + 48 AGPRs).
+// issues in the first one's stall and encoding slots.
 template <int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                                  BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
-  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t slot = slot_at(b, p);
   if (slot < 0) return;
-  const int m = b.motion ? (int)b.motion[episode_of(b, slot)] : e.motion;
-  const int m0 = __builtin_amdgcn_readfirstlane(m);
-  const int wm = __builtin_amdgcn_ballot_w64(m != m0) == 0 ? m0 : -1;
-  switch (wm) {
+  switch (wave_motion(b, p)) {
     case QT_MOTION_STATIONARY:
       rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
@@ -746,11 +769,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     case QT_MOTION_SINUSOIDAL:
       rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
-    case QT_MOTION_FIGURE8:
-      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
-      break;
     default:
-      rollout_lane<kYaw0, -1, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
   }
 }
 
@@ -759,6 +779,7 @@ inline BatchDev to_dev(const qt_batch* b) {
   d.n = b->n, d.motion = b->motion, d.pattern = b->pattern, d.plant_mass = b->plant_mass;
   d.hover = b->hover_thrust, d.K = b->K, d.k_cols = b->k_cols, d.k_per_episode = b->k_per_episode;
   d.order = b->order, d.ff = b->ff, d.slot0 = 0, d.slot_end = b->n;
+  d.nseg = 0;
   return d;
 }
 

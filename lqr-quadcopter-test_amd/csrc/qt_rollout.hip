@@ -624,8 +624,9 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 
 // One rollout launch set: the fast flavour the launch-level preconditions
 // allow, then the exact kernel for the waves it left (or for everything).
-// grouped: b covers a motion-grouped batch and the yaw-at-rest flavour runs
-// it in one launch (rollout_grouped_kernel), the exact pass with runtime motion.
+// grouped: b covers a motion-grouped batch in wave-aligned segments and the
+// yaw-at-rest flavour runs it in one launch (rollout_grouped_kernel), the exact
+// pass with runtime motion over the same slot mapping.
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                    double* rec, bool grouped = false, double* reward = nullptr) {
@@ -732,9 +733,30 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
   const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
-  if (flavor_for(batch->k_cols, ks, no_yaw, *env, *ctrl, rec) == kYaw0)  // every group in one launch
-    return launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, grid_of(batch->n), s, *env, *ctrl, *crit, b, st, nsteps,
-                          rec, true);
+  if (flavor_for(batch->k_cols, ks, no_yaw, *env, *ctrl, rec) == kYaw0) {
+    // every group in one launch, each starting at a wavefront boundary (BatchDev's
+    // wave-aligned segments; both the fast kernel and its exact pass map slots so)
+    BatchDev bg = b;
+    int64_t waves = 0, prev_end = 0;
+    bool fits = true;
+    for (int32_t i = 0; i < nseg && fits; ++i) {
+      const int64_t cnt = seg_end[i] - prev_end;
+      prev_end = seg_end[i];
+      if (cnt == 0) continue;
+      if (bg.nseg == 8) {
+        fits = false;
+        break;
+      }
+      waves += (cnt + 63) / 64;
+      bg.seg_motion[bg.nseg] = (int8_t)seg_motion[i];
+      bg.seg_end[bg.nseg] = seg_end[i];
+      bg.wave_end[bg.nseg] = waves;
+      ++bg.nseg;
+    }
+    if (fits)
+      return launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, (int)((waves * 64 + kBlock - 1) / kBlock), s, *env,
+                            *ctrl, *crit, bg, st, nsteps, rec, true);
+  }
   for (int32_t i = 0; i < nseg; ++i) {
     b.slot0 = i ? seg_end[i - 1] : 0;
     b.slot_end = seg_end[i];

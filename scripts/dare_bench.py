@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--states", default="6,9", help="state sizes to run (6, 9)")
+    ap.add_argument("--kernels", default="structured,dense", help="structured and / or dense")
     args = ap.parse_args()
 
     import numpy as np
@@ -33,7 +35,8 @@ def main():
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     m = args.m
-    for n in (6, 9):
+    kinds = [k == "structured" for k in args.kernels.split(",")]
+    for n in [int(v) for v in args.states.split(",")]:
         qd = np.concatenate([rng.uniform([5e-5, 5e-5, 10.0], [5e-4, 5e-4, 25.0], (m, 3)),
                              rng.uniform([1e-3, 1e-3, 2.0], [1e-2, 1e-2, 8.0], (m, 3))]
                             + ([rng.uniform([1e-4, 1e-4, 1e-3], [1e-3, 1e-3, 1e-2], (m, 3))] if n == 9 else []), axis=1)
@@ -45,7 +48,7 @@ def main():
         for i in range(4):
             R[i * 4 + i] = torch.from_numpy(rd[:, i])
         Q, R = Q.to(dev), R.to(dev)
-        for structured in (True, False):
+        for structured in kinds:
             core.dare_batched(n, 0.01, 9.81, None, Q[:, :256].contiguous(), R[:, :256].contiguous(), structured)
             times = []
             for _ in range(args.reps):

@@ -1,27 +1,52 @@
 #!/bin/bash
-# One GPU session: GPU tests, bench, clock stamps, kernel sweep (each step time-limited;
-# the first failure ends the script).  TAG names the output dir; STEPS selects steps.
-set -e -o pipefail
+# One GPU session (run under gpurun): the steps named in STEPS, in order, each
+# under its own time limit; the first failure ends the session.  Outputs under
+# gpurun_out/$TAG/.
+#
+#   STEPS="tests smoke bench" TAG=r03x bash scripts/gpu_session.sh
+#
+# steps:
+#   tests      pytest -m gpu (PYTEST_ARGS narrows it)
+#   smoke      __graft_entry__.smoke()
+#   bench      bench.py with the driver's defaults (BENCH_ARGS adds flags)
+#   benchab    bench.py at --steps 20 --warmup 5 and --steps 100 --warmup 20 (steadiness)
+#   workloads  scripts/run_workload.py for CONFIGS (default "3 4 5")
+#   dare       scripts/dare_bench.py (structured + dense DARE throughput)
+#   ab         scripts/ab.sh on LIBS (library builds, "tree" = in-tree) via perf_sweep
+#   clock      in-kernel clock stamps (scripts/clock_stamp.py; needs `make stamp`)
+#   profile    rocprofv3 trace + PMC passes of the bench (scripts/profile_session.sh)
+#   profw      the same for the config-3/5 workloads (scripts/profile_workloads.sh)
+#   prof       rocprofv3 trace + PMC_SETS passes of PROF_CMD (scripts/prof.sh)
+set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-run}
 mkdir -p $O
-for step in ${STEPS:-tests bench clock sweep}; do
+fail() { echo "step $1 failed"; tail -40 "$2"; exit 1; }
+for step in ${STEPS:-tests smoke bench}; do
   case $step in
-    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; } ;;
-    bench) timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err ;;
-    clock) timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 > $O/clock_linear_lqr.json 2> $O/clock.err
-           timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 --motion sinusoidal --ctl lqi > $O/clock_sin_lqi.json 2>> $O/clock.err ;;
-    sweep) timeout -k 10 300 python scripts/perf_sweep.py --n 65536 --motions ${MOTIONS:-linear,sinusoidal,circular,figure8,stationary,mixed} \
-             --ctl ${CTLS:-lqr,lqi} --reps 3 > $O/sweep.jsonl 2> $O/sweep.err ;;
-    workloads) for cfg in 3 5; do timeout -k 10 300 python scripts/run_workload.py --config $cfg >> $O/workloads.jsonl 2>> $O/workloads.err; done
-               timeout -k 10 300 python scripts/run_workload.py --config 5 --episodes 131072 >> $O/workloads.jsonl 2>> $O/workloads.err
-               timeout -k 10 300 python scripts/run_workload.py --config 4 --episodes 65536 >> $O/workloads.jsonl 2>> $O/workloads.err ;;
-    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
-    profile) TAG=${TAG:-run} timeout -k 10 900 scripts/profile_session.sh > $O/profile.log 2>&1 ;;
-    profw) TAG=${TAG:-run} timeout -k 10 900 scripts/profile_workloads.sh > $O/profw.log 2>&1 || { tail -20 $O/profw.log; exit 1; } ;;
-    dropin) timeout -k 10 300 python scripts/dropin_loop.py > $O/dropin.jsonl 2> $O/dropin.err ;;
-    dare) timeout -k 10 120 python scripts/dare_bench.py > $O/dare.jsonl 2> $O/dare.err ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+             > $O/tests.log 2>&1 || fail tests $O/tests.log
+           tail -3 $O/tests.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+           tail -1 $O/smoke.log ;;
+    bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err ;;
+    benchab) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_s20_w5.json 2> $O/benchab.err || fail benchab $O/benchab.err
+             timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline > $O/bench_s100_w20.json 2>> $O/benchab.err \
+               || fail benchab $O/benchab.err ;;
+    workloads) for c in ${CONFIGS:-3 4 5}; do
+                 timeout -k 10 300 python -u scripts/run_workload.py --config $c --repeat 10 >> $O/workloads.jsonl 2>> $O/workloads.err \
+                   || fail workloads $O/workloads.err
+               done ;;
+    dare) timeout -k 10 300 python scripts/dare_bench.py ${DARE_ARGS:-} > $O/dare.jsonl 2> $O/dare.err || fail dare $O/dare.err ;;
+    ab) timeout -k 10 600 bash scripts/ab.sh ${LIBS:-tree} > $O/ab.log 2>&1 || fail ab $O/ab.log ;;
+    clock) timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 > $O/clock_linear_lqr.json 2> $O/clock.err || fail clock $O/clock.err
+           timeout -k 10 120 python scripts/clock_stamp.py --seconds 2 --motion sinusoidal --ctl lqi > $O/clock_sin_lqi.json \
+             2>> $O/clock.err || fail clock $O/clock.err ;;
+    profile) TAG=${TAG:-run} timeout -k 10 900 bash scripts/profile_session.sh > $O/profile.log 2>&1 || fail profile $O/profile.log ;;
+    profw) TAG=${TAG:-run} timeout -k 10 900 bash scripts/profile_workloads.sh > $O/profw.log 2>&1 || fail profw $O/profw.log ;;
+    prof) TAG=${TAG:-run} timeout -k 10 900 bash scripts/prof.sh ${PROF_CMD} > $O/prof.log 2>&1 || fail prof $O/prof.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "$step done"
 done
