@@ -750,8 +750,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
 // Two waves per SIMD: mixed batches are large (config 5: 1,048,576 episodes,
 // 16 waves per SIMD on one GPU, 2 on each of 8), and a second resident wave
 // issues in the first one's stall and encoding slots.
+#ifndef QT_GROUPED_WAVES
+#define QT_GROUPED_WAVES 2
+#endif
 template <int KC, bool FF, bool KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUPED_WAVES))) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                                  BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t slot = slot_at(b, p);

@@ -71,6 +71,32 @@ class EpisodeBatch:
                             hover=col(self.hover), k_structured=self.k_structured,
                             k_no_yaw=self.k_no_yaw, ff=col(self.ff))
 
+    def physical_groups(self) -> tuple["EpisodeBatch", torch.Tensor]:
+        """For a motion-grouped batch (`order` + `groups`): a copy whose
+        per-episode arrays are stored in slot order (the groups contiguous, order
+        = None), so the grouped rollout and every kernel around it read and write
+        whole coalesced rows instead of gathering through `order` (config 5: the
+        gathered state traffic was ~5x the algorithmic bytes).  Returns (copy,
+        perm) with perm[slot] = episode; results of the copy map back with
+        `unpermute`."""
+        if self.order is None or self.groups is None:
+            raise ValueError("physical_groups needs a grouped batch (order and groups)")
+        perm = self.order.to(torch.int64)
+        col = lambda t: None if t is None else t.index_select(-1, perm).contiguous()  # noqa: E731
+        K = self.K if self.K.shape[1] == 1 else col(self.K)
+        return EpisodeBatch(n=self.n, device=self.device, pattern=col(self.pattern), offset=col(self.offset), K=K,
+                            k_cols=self.k_cols, motion=col(self.motion), plant_mass=col(self.plant_mass),
+                            hover=col(self.hover), order=None, k_structured=self.k_structured,
+                            k_no_yaw=self.k_no_yaw, groups=self.groups, ff=col(self.ff)), perm
+
+
+def unpermute(t: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """Columns (last axis) of a slot-ordered result back to episode order:
+    out[..., perm[slot]] = t[..., slot]."""
+    out = torch.empty_like(t)
+    out.index_copy_(t.dim() - 1, perm, t)
+    return out
+
 
 @dataclass
 class RolloutState:

@@ -272,18 +272,28 @@ def run_closed_loop(controller: BatchedRiccatiLQR, env_config=None, n: int | Non
     if batch is None:
         batch = build_batch(controller, cfg, n, seeds=seeds, motion=motion, plant_mass=plant_mass, draws=draws)
     crit = _criteria(criteria)
+    # a motion-grouped batch runs on its slot-ordered copy (coalesced rows);
+    # state, metrics and records come back in episode order below
+    run, perm = batch.physical_groups() if batch.groups is not None and batch.order is not None else (batch, None)
     st = core.RolloutState.empty(n, batch.device)
-    core.validate(batch, st)
-    core.reset(env, batch, st)
+    core.validate(run, st)
+    core.reset(env, run, st)
     total = max_steps if max_steps is not None else max_steps_for(env)
     step = chunk or total
     rec = torch.full((total, 16, n), float("nan"), dtype=F64, device=batch.device) if record else None
     done = 0
     while done < total:
         k = min(step, total - done)
-        core.rollout(env, controller.ctrl, crit, batch, st, k, None if rec is None else rec[done:done + k])
+        core.rollout(env, controller.ctrl, crit, run, st, k, None if rec is None else rec[done:done + k])
         done += k
     met = core.episode_metrics(crit, st)
+    if perm is not None:
+        met = core.unpermute(met, perm)
+        st = core.RolloutState(x=core.unpermute(st.x, perm), integ=core.unpermute(st.integ, perm),
+                               t=core.unpermute(st.t, perm), acc=core.unpermute(st.acc, perm),
+                               target=core.unpermute(st.target, perm))
+        if rec is not None:
+            rec = core.unpermute(rec, perm)
     return RolloutResult(metrics=met, state=st, batch=batch, criteria=crit, record=rec, env=env,
                          ctrl=controller.ctrl)
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 kernel trace + one SQ counter pass for the secondary workloads:
+# rocprofv3 kernel trace + SQ counter and HBM (FETCH_SIZE, WRITE_SIZE) passes for the secondary workloads:
 # config 3 (LQI, sinusoidal), config 5 (1M episodes, grouped motions, one
 # launch), and the batched DARE kernels (scripts/dare_bench.py).  Every step is
 # time-limited; the first failure ends the script.  Outputs under
@@ -15,14 +15,19 @@ run_case() {  # name, then the python arguments
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${name}_trace -o run -- python3 "$@" \
     > $OUT/${name}_trace.log 2>&1 || { echo "$name trace failed"; tail -20 $OUT/${name}_trace.log; exit 1; }
-  timeout -k 10 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/${name}_sq -o run -- python3 "$@" \
-    > $OUT/${name}_sq.log 2>&1 || { echo "$name sq failed"; tail -20 $OUT/${name}_sq.log; exit 1; }
+  local pass=0
+  IFS=';' read -ra SETS <<< "${PMC_SETS:-$SQ;FETCH_SIZE;WRITE_SIZE}"
+  for PMC in "${SETS[@]}"; do
+    pass=$((pass + 1))
+    timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${name}_pmc$pass -o run -- python3 "$@" \
+      > $OUT/${name}_pmc$pass.log 2>&1 || { echo "$name pmc $PMC failed"; tail -20 $OUT/${name}_pmc$pass.log; exit 1; }
+  done
   echo "$name done"
 }
 for c in ${CASES:-cfg3 cfg5 dare}; do
   case $c in
     cfg3) run_case cfg3 scripts/run_workload.py --config 3 --repeat 10 ;;
     cfg5) run_case cfg5 scripts/run_workload.py --config 5 --repeat 5 ;;
-    dare) run_case dare scripts/dare_bench.py --reps 5 ;;
+    dare) run_case dare scripts/dare_bench.py --reps 5 ${DARE_ARGS:-} ;;
   esac
 done

@@ -74,6 +74,10 @@ def main():
     t_batch_warm = time.perf_counter() - t0
     del sh2
 
+    # a grouped batch runs on its slot-ordered copy, as run_closed_loop does (coalesced rows)
+    perm = None
+    if batch.groups is not None and batch.order is not None:
+        batch, perm = batch.physical_groups()
     env = sh.env_config.to_params()
     crit = _criteria(None)
     st = core.RolloutState.empty(sh.n, dev)
@@ -95,6 +99,8 @@ def main():
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     met = core.episode_metrics(crit, st)
+    if perm is not None:
+        met = core.unpermute(met, perm)
     steps = met[MET["steps"]].sum()
     if world > 1:
         dist.all_reduce(steps)
