@@ -391,8 +391,10 @@ def pmc_traffic(kernel_tags):
                    if os.path.exists(os.path.join(d, "pmc_FETCH_SIZE.csv"))), reverse=True)
 
     def avg(path, counter, tag):
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if r["Counter_Name"] == counter and tag in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter and tag in r["Kernel_Name"]]
+        if rows and "Average_Per_Dispatch" in rows[0]:  # scripts/pmc_summary.py form (round 3 on)
+            return float(rows[0]["Average_Per_Dispatch"])
+        vals = [float(r["Counter_Value"]) for r in rows]  # rocprofv3's per-dispatch rows
         return sum(vals) / len(vals) if vals else None
 
     for d in dirs:
