@@ -1,20 +1,23 @@
 #!/usr/bin/env python3
 """Block / branch map of one rollout kernel's step loop from a gfx950 .s dump
-(hipcc --cuda-device-only -S csrc/qt_rollout.hip).  Used to check that the
-fast step's common path has no taken branch but the loop back-edge.
+(`make -C lqr-quadcopter-test_amd asm`).  Used to check that the fast step's
+common path has no taken branch but the loop back-edge.
 
   python scripts/loop_blocks.py <file.s> [mangled-name-fragment]
+  python scripts/loop_blocks.py <file.s> --table
+
+--table lists the step-loop body (instructions / VALU / SALU) of every
+yaw-at-rest rollout_kernel instance and every per-motion loop of
+rollout_grouped_kernel: the instructions one wave issues per env step.
 """
 
 import re
 import sys
 
+MOTIONS = {"0": "stationary", "1": "linear", "2": "circular", "3": "sinusoidal", "4": "figure8", "n1": "runtime"}
 
-def main():
-    path = sys.argv[1]
-    tag = sys.argv[2] if len(sys.argv) > 2 else "ILi2ELi1ELi6ELb0ELb1E"  # yaw-at-rest, linear, K6, no FF, KS
-    s = open(path).read()
-    name = [m for m in re.findall(r"^(_Z\S*rollout_kernel\S*):", s, re.M) if tag in m][0]
+
+def blocks_of(s, name):
     body = s[s.index(name + ":"):]
     body = body[:body.index(".Lfunc_end")]
     blocks, cur = [], None
@@ -22,7 +25,7 @@ def main():
         t = line.strip()
         if re.match(r"^\.LBB\S+:", t) or t.startswith("; %bb."):
             cur = {"name": t.split()[0].rstrip(":"), "loop": "Loop" in t, "hdr": "=>This Loop Header" in t,
-                   "n": 0, "valu": 0, "salu": 0, "br": []}
+                   "inner": "Parent Loop" in t, "n": 0, "valu": 0, "salu": 0, "br": []}
             blocks.append(cur)
             continue
         if cur is None or not t or t.startswith((";", ".")):
@@ -33,7 +36,41 @@ def main():
         cur["salu"] += op.startswith("s_")
         if op.startswith(("s_cbranch", "s_branch")):
             cur["br"].append(t.split(";")[0].strip())
-    for b in blocks:
+    return blocks
+
+
+def step_loops(blocks):
+    """Single-block step loops: a block whose last branch jumps to itself."""
+    return [b for b in blocks if b["br"] and b["br"][-1].endswith(" " + b["name"]) and b["n"] > 100]
+
+
+def table(s):
+    print(f"{'kernel':46s} {'motion':11s} {'instr':>5s} {'VALU':>5s} {'SALU':>5s}")
+    for name in re.findall(r"^(_Z\S*rollout_kernel\S*):", s, re.M):
+        m = re.search(r"rollout_kernelILi(\d)ELi(n?\d)ELi(\d)ELb(\d)ELb(\d)ELb(\d)E", name)
+        if not m or m.group(1) != "2":
+            continue
+        fl, mo, kc, ff, ks, uni = m.groups()
+        for b in step_loops(blocks_of(s, name)):
+            tag = f"rollout_kernel<2,{mo.replace('n', '-')},{kc},ff{ff},ks{ks},uni{uni}>"
+            print(f"{tag:46s} {MOTIONS[mo]:11s} {b['n']:5d} {b['valu']:5d} {b['salu']:5d}")
+    for name in re.findall(r"^(_Z\S*rollout_grouped_kernel\S*):", s, re.M):
+        m = re.search(r"rollout_grouped_kernelILi(\d)ELb(\d)ELb(\d)E", name)
+        kc, ff, ks = m.groups()
+        # the per-motion loops appear in the switch order of rollout_grouped_kernel
+        for b in step_loops(blocks_of(s, name)):
+            tag = f"rollout_grouped_kernel<{kc},ff{ff},ks{ks}>"
+            print(f"{tag:46s} {'(a motion)':11s} {b['n']:5d} {b['valu']:5d} {b['salu']:5d}")
+
+
+def main():
+    path = sys.argv[1]
+    s = open(path).read()
+    if len(sys.argv) > 2 and sys.argv[2] == "--table":
+        return table(s)
+    tag = sys.argv[2] if len(sys.argv) > 2 else "ILi2ELi1ELi6ELb0ELb1E"  # yaw-at-rest, linear, K6, no FF, KS
+    name = [m for m in re.findall(r"^(_Z\S*rollout_kernel\S*):", s, re.M) if tag in m][0]
+    for b in blocks_of(s, name):
         if b["loop"] or b["hdr"]:
             mark = "H" if b["hdr"] else " "
             print(f"{mark} {b['name']:14s} n={b['n']:4d} valu={b['valu']:4d} salu={b['salu']:3d} {b['br']}")

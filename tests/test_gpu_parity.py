@@ -550,6 +550,45 @@ def test_general_dare_random_systems(qt):
         np.testing.assert_allclose(K, np.linalg.solve(R + BtP @ B, BtP @ A), rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("n,p", [(1, 1), (3, 8), (16, 1), (16, 8), (10, 6)])
+def test_dense_dare_batch_edge_sizes(qt, n, p):
+    """The dense group kernel at its size limits (n <= 16, p <= 8, every
+    group-size branch of launch_dare_group) on a ragged batch of 67 random
+    problems (not a multiple of the problems per wave): every problem
+    satisfies its own DARE and K = (R + B'PB)^-1 B'PA; sizes outside the
+    limits are refused."""
+    from quadtrack import core, solve_dare
+
+    rng = np.random.default_rng(100 * n + p)
+    m = 67
+    A = rng.normal(size=(m, n, n)) * (0.4 / np.sqrt(n)) + np.eye(n) * 0.6
+    B = rng.normal(size=(m, n, p))
+    M = rng.normal(size=(m, n, n))
+    Q = M @ M.transpose(0, 2, 1) + np.eye(n) * 0.1
+    L = rng.normal(size=(m, p, p)) * 0.3
+    R = L @ L.transpose(0, 2, 1) + np.eye(p)
+    dev = torch.device("cuda:0")
+
+    def soa(x):
+        return torch.as_tensor(np.ascontiguousarray(x.reshape(m, -1).T), device=dev)
+
+    K, P, st, it = core.dare_dense(soa(A), soa(B), soa(Q), soa(R), ab_per_problem=True)
+    assert st.cpu().tolist() == [0] * m
+    K = K.cpu().numpy().T.reshape(m, p, n)
+    P = P.cpu().numpy().T.reshape(m, n, n)
+    for i in range(m):
+        a, b, q, r, pp = A[i], B[i], Q[i], R[i], P[i]
+        btp = b.T @ pp
+        res = a.T @ pp @ a - pp - a.T @ pp @ b @ np.linalg.solve(r + btp @ b, btp @ a) + q
+        assert np.max(np.abs(res)) <= 1e-9 * max(1.0, np.max(np.abs(pp))), (i, np.max(np.abs(res)))
+        np.testing.assert_allclose(K[i], np.linalg.solve(r + btp @ b, btp @ a), rtol=1e-8, atol=1e-11,
+                                   err_msg=str(i))
+    with pytest.raises(ValueError, match="n <= 16"):
+        solve_dare(np.eye(17), np.ones((17, 1)), np.eye(17), np.eye(1))
+    with pytest.raises(ValueError, match="m <= 8"):
+        solve_dare(np.eye(2), np.ones((2, 9)), np.eye(2), np.eye(9))
+
+
 # ------------------------------------------------------- component kernels
 
 
