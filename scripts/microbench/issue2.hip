@@ -137,6 +137,56 @@ __global__ __launch_bounds__(256) void k_rsq(double* out, Stamp* st, double a, d
   stamp_out(st, t0, r0, x + y + z + w, out);
 }
 
+// + 1 v_rsq_f64 whose result is first read 16 FMAs later (latency hidden,
+// only its issue cost left)
+__global__ __launch_bounds__(256) void k_rsq_late(double* out, Stamp* st, double a, double b, int half) {
+  PROLOGUE
+  double r = 1.0;
+  for (int i = 0; i < kIters; ++i) {
+    asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(r));
+    asm volatile("v_rsq_f64 %0, %1" : "=&v"(r) : "v"(w));
+    FMA4; FMA4; FMA4; FMA4;
+  }
+  stamp_out(st, t0, r0, x + y + z + w, out);
+}
+
+// + 1 v_sqrt_f64 whose result is first read 16 FMAs later
+__global__ __launch_bounds__(256) void k_sqrt_late(double* out, Stamp* st, double a, double b, int half) {
+  PROLOGUE
+  double r = 1.0;
+  for (int i = 0; i < kIters; ++i) {
+    asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(r));
+    asm volatile("v_sqrt_f64 %0, %1" : "=&v"(r) : "v"(w));
+    FMA4; FMA4; FMA4; FMA4;
+  }
+  stamp_out(st, t0, r0, x + y + z + w, out);
+}
+
+// + 1 v_rcp_f64 whose result is first read 16 FMAs later
+__global__ __launch_bounds__(256) void k_rcp_late(double* out, Stamp* st, double a, double b, int half) {
+  PROLOGUE
+  double r = 1.0;
+  for (int i = 0; i < kIters; ++i) {
+    asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(r));
+    asm volatile("v_rcp_f64 %0, %1" : "=&v"(r) : "v"(w));
+    FMA4; FMA4; FMA4; FMA4;
+  }
+  stamp_out(st, t0, r0, x + y + z + w, out);
+}
+
+// + 1 v_fma_f64 whose result feeds the very next FMA (FP64 dependency latency)
+__global__ __launch_bounds__(256) void k_fmadep(double* out, Stamp* st, double a, double b, int half) {
+  PROLOGUE
+  double r;
+  for (int i = 0; i < kIters; ++i) {
+    FMA4; FMA4;
+    asm volatile("v_fma_f64 %0, %1, %2, %3\nv_fma_f64 %0, %0, %2, %3" : "=&v"(r) : "v"(w), "v"(a), "v"(b));
+    asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(r));
+    FMA4; FMA4;
+  }
+  stamp_out(st, t0, r0, x + y + z + w, out);
+}
+
 // + v_cmp_f64 (writes VCC) feeding 2 v_cndmask_b32 (a double select)
 __global__ __launch_bounds__(256) void k_sel(double* out, Stamp* st, double a, double b, int half) {
   PROLOGUE
@@ -162,7 +212,8 @@ int main() {
     int extra;  // non-FMA instructions per iteration
   } ks[] = {{"fma16", k_fma, 0},          {"fma16+4salu", k_salu, 4}, {"fma16+branch", k_branch, 1},
             {"fma16+cbranch_nt", k_nobranch, 2}, {"fma16+4mov64", k_mov64, 4}, {"fma16+4b32", k_b32, 4},
-            {"fma16+rsq(dep)", k_rsq, 3},  {"fma16+cmp+2cndmask", k_sel, 3}};
+            {"fma16+rsq(dep)", k_rsq, 3}, {"fma16+rsq(late)", k_rsq_late, 2}, {"fma16+sqrt(late)", k_sqrt_late, 2},
+            {"fma16+rcp(late)", k_rcp_late, 2}, {"fma16+fma2dep+add", k_fmadep, 3},  {"fma16+cmp+2cndmask", k_sel, 3}};
   const int maxw = 4096;
   double* out;
   Stamp* st;
