@@ -393,7 +393,7 @@ def summary_partials(met: torch.Tensor, mu_ratio=0.0, mu_err=0.0, nparts: int | 
     lib = _abi.load()
     n = met.shape[1]
     nparts = summary_parts_for(n) if nparts is None else int(nparts)
-    out = torch.zeros(11, dtype=F64, device=met.device)
+    out = torch.empty(11, dtype=F64, device=met.device)  # the final reduction writes all 11
     with torch.cuda.device(met.device):
         if nparts == 1:
             check(lib.qt_summary(n, ptr(met), float(mu_ratio), float(mu_err), ptr(out), stream_of(met.device)),
