@@ -327,11 +327,18 @@ def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: Epi
               "qt_rollout_rewards")
 
 
-def motion_groups(motion: np.ndarray):
-    """Host grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end)."""
-    motion = np.asarray(motion).reshape(-1)
-    order = np.argsort(motion, kind="stable").astype(np.int32)
-    counts = np.bincount(motion.astype(np.intp), minlength=5)  # motion types 0..4: O(n), no sort
+def motion_groups(motion):
+    """Grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end).
+    A device tensor of motion types is grouped on the device (stable sort, one
+    5-element read back); a numpy array on the host."""
+    if isinstance(motion, torch.Tensor):
+        m = motion.reshape(-1)
+        order = torch.argsort(m, stable=True).to(torch.int32)
+        counts = torch.bincount(m.to(torch.int64), minlength=5).cpu().numpy()
+    else:
+        m = np.asarray(motion).reshape(-1)
+        order = np.argsort(m, kind="stable").astype(np.int32)
+        counts = np.bincount(m.astype(np.intp), minlength=5)  # motion types 0..4: O(n), no sort
     kinds = np.nonzero(counts)[0]
     return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts[kinds])]
 

@@ -236,7 +236,7 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
     mo = None if kinds is None else torch.as_tensor(kinds, device=dev)
     groups = None
     if kinds is not None and order is None and group_motion and kinds.size and np.any(kinds != kinds.flat[0]):
-        order, seg_motion, seg_end = core.motion_groups(kinds)
+        order, seg_motion, seg_end = core.motion_groups(mo)  # on the device: the order stays there
         groups = (seg_motion, seg_end)
     if plant_mass is None:
         pm = None
@@ -244,7 +244,12 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
         pm = core.to_device(plant_mass.reshape(-1), dev)
     else:
         pm = core.to_device(np.broadcast_to(np.asarray(plant_mass, float), (n,)), dev)
-    od = None if order is None else torch.as_tensor(np.asarray(order, dtype=np.int32), device=dev)
+    if order is None:
+        od = None
+    elif isinstance(order, torch.Tensor):
+        od = order.to(device=dev, dtype=torch.int32)
+    else:
+        od = torch.as_tensor(np.asarray(order, dtype=np.int32), device=dev)
     b = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pat, dev), offset=core.to_device(off, dev),
                           K=controller.K, k_cols=controller.k_cols, motion=mo, plant_mass=pm, hover=controller.hover,
                           order=od, k_structured=controller.k_structured,

@@ -108,7 +108,9 @@ def episode_masses(lo: int, hi: int, device) -> torch.Tensor:
 
 
 def motion_of(lo: int, hi: int) -> np.ndarray:
-    return (np.arange(lo, hi) % 5).astype(np.int8)
+    """Motion type i mod 5 of episodes [lo, hi) (the 5-cycle tiled, no 64-bit modulo)."""
+    n = max(0, hi - lo)
+    return np.tile(((np.arange(5) + lo) % 5).astype(np.int8), -(-n // 5))[:n]
 
 
 def build(config: int, lo: int | None = None, hi: int | None = None, device=None) -> Shard:

@@ -75,9 +75,14 @@ def main():
     del sh2
 
     # a grouped batch runs on its slot-ordered copy, as run_closed_loop does (coalesced rows)
-    perm = None
+    perm, t_copy = None, None
     if batch.groups is not None and batch.order is not None:
+        batch.physical_groups()  # first call: allocator and kernels warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         batch, perm = batch.physical_groups()
+        torch.cuda.synchronize()
+        t_copy = time.perf_counter() - t0
     env = sh.env_config.to_params()
     crit = _criteria(None)
     st = core.RolloutState.empty(sh.n, dev)
@@ -117,7 +122,8 @@ def main():
             "config": args.config, "episodes": total, "world": world, "episodes_per_rank": sh.n,
             "grouped": batch.groups is not None,
             "setup_s": {"controller_dare_and_params": round(t_ctl, 4), "batch_draws": round(t_batch, 4)},
-            "setup_warm_s": {"controller_dare_and_params": round(t_ctl_warm, 4), "batch_draws": round(t_batch_warm, 4)},
+            "setup_warm_s": {"controller_dare_and_params": round(t_ctl_warm, 4), "batch_draws": round(t_batch_warm, 4),
+                             "group_copy": None if t_copy is None else round(t_copy, 4)},
             "dare_max_iterations": int(sh.controller.iters.max().item()),
             "dare_fallbacks": int((sh.controller.status != 0).sum().item()),
             "rollout_ms": round(kern, 3), "rollout_ms_median": round(sorted(times)[len(times) // 2], 3),
