@@ -483,10 +483,58 @@ QT_HD VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
 // angle theta_i = omega_i t + phase_i advances by the fixed rotation
 // (cos, sin)(fl(omega_i dt)) and omega_i times the time step's rounding each
 // step (qt_kernels.hpp, Rotor).
+// Safe horizon of the yaw-at-rest loop (run_yaw0, yaw0_horizon): uniform
+// bounds on how far one step can move the quantities the loop's stop vote
+// tests, so that a wave can run the steps no lane can stop at without the
+// vote.  Per step, with |T| <= tmax (the controller's thrust clip) and every
+// stage thrust direction a unit vector (integrate_yaw0):
+//   speed     |v'| <= cv |v| + |T| / m sum_i |wv_i| + |gv|   (0 <= cv <= 1)
+//   position  |p'_j - p_j| <= |pv| vmax + |T| / m sum_i |pa_i| + |gp|
+//   tilt      |a' - a| <= (|ay| + |au|) max_rate   (rate-bounded: |w|, |u| <= max_rate)
+//   time      t' - t <= dt + the rounding of t + dt
+// each widened by `slack` (relative) and an absolute term for the rounding of
+// the step's few operations.  on == 0 (a non-finite or non-positive limit):
+// no horizon, the loop votes every step.
+struct Horizon {
+  int on;
+  double tmax;       // max(|min_thrust|, |max_thrust|) of the controller
+  double vmax;       // max_velocity (1 - 1e-12): the speed bound kept below the vote's
+  double vmax2;      // vmax^2
+  double inv_2vmax;  // 1 / (2 vmax): (vmax^2 - |v|^2) / (2 vmax) <= vmax - |v|
+  double vabs;       // absolute slack per step on the speed bound
+  double pmax;       // max_position
+  double pabs;       // absolute slack per step on a position
+  double inv_dang;   // 1 / per-step tilt bound
+  double inv_tstep;  // 1 / per-step time bound
+  double slack;      // relative widening of the per-lane step bounds
+};
+
+QT_HD Horizon make_horizon(const qt_env_params& e, const qt_ctrl_params& c, const RateLin& rl) {
+  Horizon h{};
+  const double tm = fmax(fabs(c.min_thrust), fabs(c.max_thrust));
+  const bool ok = e.max_velocity > 0.0 && e.max_velocity < 1e150 && e.max_position > 0.0 &&
+                  e.max_position < 1e150 && e.dt > 0.0 && e.dt < 1e3 && fabs(e.max_episode_time) < 1e150 &&
+                  tm < 1e150 && c.max_rate >= 0.0 && c.max_rate < 1e150;
+  if (!ok) return h;
+  h.on = 1;
+  h.tmax = tm;
+  h.vmax = e.max_velocity * (1.0 - 1e-12);
+  h.vmax2 = h.vmax * h.vmax;
+  h.inv_2vmax = 1.0 / (2.0 * h.vmax);
+  h.vabs = e.max_velocity * 1e-14;
+  h.pmax = e.max_position;
+  h.pabs = e.max_position * 1e-15 + 1e-300;
+  h.inv_dang = 1.0 / ((fabs(rl.ay) + fabs(rl.au)) * c.max_rate * (1.0 + 1e-9) + 2e-15);
+  h.inv_tstep = 1.0 / ((e.dt + (fabs(e.max_episode_time) + e.dt) * 4.5e-16) * (1.0 + 1e-9));
+  h.slack = 1.0 + 1e-9;
+  return h;
+}
+
 struct LaunchConst {
   RateLin rl;
   VelLin vl;
   Plant pl;
+  Horizon hz;
   double rc[5][3], rs[5][3];  // per motion type: cos / sin of fl(omega_i dt)
   double om[5][3];            // per motion type: omega_i
   // deferred-wave flag of this launch set (per stream, qt_rollout.hip): a

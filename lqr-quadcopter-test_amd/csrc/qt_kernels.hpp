@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "qt_device.hpp"
 
 
@@ -466,6 +468,46 @@ __device__ __forceinline__ void tilt_clamp(double* x, Trig& ta) {
   }
 }
 
+// Safe horizon of the yaw-at-rest loop: an even number H of steps (wave-
+// uniform, 0 <= H <= kMaxHorizon, H <= rem - 1) that no active lane of the
+// wave can stop at, so the wave runs them without the stop vote.  Each lane
+// bounds its distance to every stop condition the vote tests by the per-step
+// bounds of Horizon (LaunchConst::hz): speed from the velocity clamp's guard,
+// the position bound, (TILT) roll / pitch from the tilt clamp, the time limit;
+// the wave takes the minimum over its active lanes by ballots (inactive lanes
+// cast no vote).  The bounds hold for the state the loop is in at every
+// step start (finite, |v| below the clamp, |w| and |u| within max_rate:
+// rate_bounded_ok), so a no-vote step is exactly a voted step that did not
+// stop.  H = 0 (one voted step) when the wave is near a stop or hz.on == 0.
+constexpr int kMaxHorizon = 62;
+constexpr int kVotedBurst = 4;
+
+template <bool TILT>
+__device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizon& hz, const VelLin& lin,
+                                            const Plant& pl, const double* x, double t, int rem) {
+  const double tmi = hz.tmax * pl.inv_mass;
+  const double sw = (fabs(lin.wv[0]) + fabs(lin.wv[1])) + (fabs(lin.wv[2]) + fabs(lin.wv[3]));
+  const double spa = (fabs(lin.pa[0]) + fabs(lin.pa[1])) + fabs(lin.pa[2]);
+  const double dv = fma(fma(tmi, sw, fabs(lin.gv)), hz.slack, hz.vabs);                        // speed per step
+  const double dp = fma(fma(fabs(lin.pv), hz.vmax, fma(tmi, spa, fabs(lin.gp))), hz.slack, hz.pabs);  // position
+  // speed: (vmax^2 - |v|^2) / (2 vmax) <= vmax - |v| (no square root)
+  const double s = fma(x[5], x[5], fma(x[4], x[4], x[3] * x[3]));
+  double h = (hz.vmax2 - s) * hz.inv_2vmax * __builtin_amdgcn_rcp(dv);
+  h = fmin(h, (hz.pmax - fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2])))) * __builtin_amdgcn_rcp(dp));
+  if (TILT) h = fmin(h, (kMaxTilt - fmax(fabs(x[6]), fabs(x[7]))) * hz.inv_dang);
+  h = fmin(h, (e.max_episode_time - t) * hz.inv_tstep);
+  // rcp's error (well below 1e-6) and the step about to be voted on
+  h = fma(h, 1.0 - 1e-6, -1.0);
+  const bool lane_ok = h >= 2.0 && lin.cv >= 0.0 && lin.cv <= 1.0;
+  const int hl = lane_ok ? (int)fmin(h, (double)kMaxHorizon) : 0;
+  int H = 0;
+#pragma unroll
+  for (int bit = 32; bit >= 2; bit >>= 1)
+    if (__builtin_amdgcn_ballot_w64(hl < H + bit) == 0) H += bit;
+  const int rcap = (rem - 1) & ~1;
+  return hz.on ? (H < rcap ? H : rcap) : 0;
+}
+
 // The yaw-at-rest fast loop (flavour kYaw0).  One wave-uniform loop: every
 // step runs branch-free (closed-form RK4, carried roll / pitch and target
 // trig, fused metrics) and ends with ONE wave vote; the loop leaves only when
@@ -518,18 +560,21 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   double cur = a.os_cur;
   int on_pre = a.on_pre, on_post = a.on_post, os_count = a.os_count;
   bool stepped = false;
-  // Where the tilt clamp goes (the same arithmetic either way): LQI runs can
-  // diverge and hold their tilt at the clamp, so their loop
-  // applies it every step; the others stop the loop at a clamping step (rare
-  // for them) and apply it after, which spares the loop its ~10 operations.
-  constexpr bool kTiltVote = KC != 9;
-  const double tilt_up = nextafter(kMaxTilt, INFINITY);  // |a| > kMaxTilt as a >= test
+  // Where the tilt clamp goes (the same arithmetic either way): every voted
+  // step applies it; the horizon's steps skip it where the horizon also bounds
+  // the tilt (kTiltHorizon), which spares them its ~10 operations.  LQI runs
+  // can diverge and hold their tilt at the clamp, so a tilt bound
+  // would keep their horizon at zero: their horizon leaves the tilt out and
+  // every step applies the clamp.
+  constexpr bool kTiltHorizon = KC != 9;
   int s = 0;
   while (a.term == QT_TERM_RUNNING && s < nsteps) {
     const int s0 = s;
     int rem = nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0;  // steps left in this run (z stays < 1 off phase)
     RateCoef rk;
-    do {
+    // one closed-loop step; VOTE: end it with the stop vote (true: stop here)
+    auto step = [&](auto vote) -> bool {
+      constexpr bool VOTE = decltype(vote)::value;
       rk.pin();
       const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_resid)
       // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -580,34 +625,46 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       // angle wrap (no correction: tilt-bounded), carried roll / pitch trig of
       // the wrapped angles (attitude_trig_resid's bound holds for them), then
       // the tilt clamp on both the angles and their trig (tilt_clamp): here,
-      // or after the loop, which a tilt beyond the clamp then stops (kTiltVote)
+      // in every voted step and (!kTiltHorizon) in the horizon's steps too
       if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
       attitude_trig_resid(x + 6, a0, d4, t4, ta);
-      if (!kTiltVote && !(QT_ABLATE & QT_ABL_CONSTRAIN)) tilt_clamp(x, ta);
+      if ((VOTE || !kTiltHorizon) && !(QT_ABLATE & QT_ABL_CONSTRAIN)) tilt_clamp(x, ta);
       // the stop conditions as one maximum >= 0 (the state is finite): speed
       // at the clamp's guard band, position bounds, time limit, end of the run
-      // (rem, uniform), kTiltVote: tilt beyond its clamp — one compare and one
+      // (rem, uniform) — one compare and one
       // ballot straight into the branch, no serial scalar chain at the end of
       // the step
+      if constexpr (!VOTE) return false;
       --rem;
       double stop_m =
           fmax(fmax(fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) - pos_up, (x[3] * x[3] + x[4] * x[4] + x[5] * x[5]) - vm2),
                fmax(t - e.max_episode_time, -(double)rem));
-      if (kTiltVote) stop_m = fmax(stop_m, fmax(fabs(x[6]), fabs(x[7])) - tilt_up);
-      if (__builtin_amdgcn_ballot_w64(stop_m >= 0.0)) break;
+      return __builtin_amdgcn_ballot_w64(stop_m >= 0.0) != 0;
+    };
+    // The safe horizon's steps without the vote (in pairs: one back edge per
+    // two steps), then one voted step.
+    do {
+      const int H = yaw0_horizon<kTiltHorizon>(e, k.hz, lin, pl, x, t, rem);
+      for (int j = 0; j < H; j += 2) {
+        step(std::false_type{});
+        step(std::false_type{});
+      }
+      rem -= H;
+      // a wave with a lane near a stop (H = 0) takes a few voted steps before
+      // it bounds the horizon again
+      const int nv = H > 0 ? 1 : kVotedBurst;
+      bool stop = false;
+      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{});
+      if (stop) break;
     } while (true);
     const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;
     s += ran;
     a.steps += ran;
     stepped = true;
     z = z <= 0 ? kNeg : z;  // off phase: keep z far below 1 for the next run
-    // finish the last step exactly: the velocity and (kTiltVote) tilt clamps
-    // where they act, per-lane termination (all no-ops for a lane the vote did
-    // not stop)
-    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) {
-      clamp_velocity(e, x);
-      if (kTiltVote && (fabs(x[6]) > kMaxTilt || fabs(x[7]) > kMaxTilt)) tilt_clamp(x, ta);
-    }
+    // finish the last step exactly: the velocity clamp where it acts and
+    // per-lane termination (no-ops for a lane the vote did not stop)
+    if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) clamp_velocity(e, x);
     a.term = (QT_ABLATE & QT_ABL_TERMINATION) ? (t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING)
                                                : termination_fast(e, t, x);
   }

@@ -631,6 +631,7 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                    double* rec, bool grouped = false, double* reward = nullptr) {
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
+  lc.hz = make_horizon(e, c, lc.rl);       // the yaw-at-rest loop's safe horizon
   lc.reward = reward;
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;

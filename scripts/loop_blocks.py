@@ -6,9 +6,10 @@ common path has no taken branch but the loop back-edge.
   python scripts/loop_blocks.py <file.s> [mangled-name-fragment]
   python scripts/loop_blocks.py <file.s> --table
 
---table lists the step-loop body (instructions / VALU / SALU) of every
-yaw-at-rest rollout_kernel instance and every per-motion loop of
-rollout_grouped_kernel: the instructions one wave issues per env step.
+--table lists, for every yaw-at-rest rollout_kernel instance and every
+per-motion loop of rollout_grouped_kernel, the instructions one wave issues
+per env step inside the safe horizon (the two-step no-vote loop, halved) and
+in the voted step that ends each horizon (run_yaw0).
 """
 
 import re
@@ -40,27 +41,39 @@ def blocks_of(s, name):
 
 
 def step_loops(blocks):
-    """Single-block step loops: a block whose last branch jumps to itself."""
-    return [b for b in blocks if b["br"] and b["br"][-1].endswith(" " + b["name"]) and b["n"] > 100]
+    """The horizon's two-step body (a self-looping block of > 100 instructions
+    whose back edge tests a scalar count) with the voted step after it (the
+    next block of > 100 instructions whose branch tests the vote, vcc)."""
+    out = []
+    big = [b for b in blocks if b["n"] > 100]
+    for i, b in enumerate(big):
+        if any(br.endswith(" " + b["name"]) for br in b["br"]) and not any("vcc" in br for br in b["br"]):
+            voted = next((v for v in big[i + 1:] if any("vcc" in br for br in v["br"])), None)
+            out.append((b, voted))
+    return out
+
+
+def row(tag, motion, pair, voted):
+    v = f"{voted['n']:5d} {voted['valu']:5d} {voted['salu']:5d}" if voted else "    -     -     -"
+    print(f"{tag:46s} {motion:11s} {pair['n'] / 2:6.1f} {pair['valu'] / 2:6.1f} {pair['salu'] / 2:5.1f}   {v}")
 
 
 def table(s):
-    print(f"{'kernel':46s} {'motion':11s} {'instr':>5s} {'VALU':>5s} {'SALU':>5s}")
+    print(f"{'kernel':46s} {'motion':11s} {'per no-vote step':>19s}   {'voted step':>17s}")
+    print(f"{'':46s} {'':11s} {'instr':>6s} {'VALU':>6s} {'SALU':>5s}   {'instr':>5s} {'VALU':>5s} {'SALU':>5s}")
     for name in re.findall(r"^(_Z\S*rollout_kernel\S*):", s, re.M):
         m = re.search(r"rollout_kernelILi(\d)ELi(n?\d)ELi(\d)ELb(\d)ELb(\d)ELb(\d)E", name)
         if not m or m.group(1) != "2":
             continue
         fl, mo, kc, ff, ks, uni = m.groups()
-        for b in step_loops(blocks_of(s, name)):
-            tag = f"rollout_kernel<2,{mo.replace('n', '-')},{kc},ff{ff},ks{ks},uni{uni}>"
-            print(f"{tag:46s} {MOTIONS[mo]:11s} {b['n']:5d} {b['valu']:5d} {b['salu']:5d}")
+        for pair, voted in step_loops(blocks_of(s, name)):
+            row(f"rollout_kernel<2,{mo.replace('n', '-')},{kc},ff{ff},ks{ks},uni{uni}>", MOTIONS[mo], pair, voted)
     for name in re.findall(r"^(_Z\S*rollout_grouped_kernel\S*):", s, re.M):
         m = re.search(r"rollout_grouped_kernelILi(\d)ELb(\d)ELb(\d)E", name)
         kc, ff, ks = m.groups()
         # the per-motion loops appear in the switch order of rollout_grouped_kernel
-        for b in step_loops(blocks_of(s, name)):
-            tag = f"rollout_grouped_kernel<{kc},ff{ff},ks{ks}>"
-            print(f"{tag:46s} {'(a motion)':11s} {b['n']:5d} {b['valu']:5d} {b['salu']:5d}")
+        for pair, voted in step_loops(blocks_of(s, name)):
+            row(f"rollout_grouped_kernel<{kc},ff{ff},ks{ks}>", "(a motion)", pair, voted)
 
 
 def main():
