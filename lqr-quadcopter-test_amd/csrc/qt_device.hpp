@@ -507,6 +507,11 @@ struct Horizon {
   double inv_dang;   // 1 / per-step tilt bound
   double inv_tstep;  // 1 / per-step time bound
   double slack;      // relative widening of the per-lane step bounds
+  // The one binade of t in which t + dt rounds to a tie (dt's lowest set bit
+  // is half an ulp of t there: round-half-even then alternates the step),
+  // as the biased-exponent bits of t; elsewhere fl(t + dt) - t is the same
+  // for every t of a binade (t is a multiple of its ulp).
+  long long tie_exp_bits;
 };
 
 QT_HD Horizon make_horizon(const qt_env_params& e, const qt_ctrl_params& c, const RateLin& rl) {
@@ -527,6 +532,16 @@ QT_HD Horizon make_horizon(const qt_env_params& e, const qt_ctrl_params& c, cons
   h.inv_dang = 1.0 / ((fabs(rl.ay) + fabs(rl.au)) * c.max_rate * (1.0 + 1e-9) + 2e-15);
   h.inv_tstep = 1.0 / ((e.dt + (fabs(e.max_episode_time) + e.dt) * 4.5e-16) * (1.0 + 1e-9));
   h.slack = 1.0 + 1e-9;
+  {
+    // dt = m 2^q with m odd: the lowest set bit 2^q is half an ulp of t
+    // for t in [2^(q + 53), 2^(q + 54))
+    int q = 0;
+    double m = frexp(e.dt, &q) * 9007199254740992.0;  // 53-bit integer mantissa, dt = m 2^(q - 53)
+    q -= 53;
+    while (fmod(m, 2.0) == 0.0) m *= 0.5, ++q;
+    const long long be = (long long)(q + 53) + 1023;
+    h.tie_exp_bits = (be > 0 && be < 2047) ? (be << 52) : -1;
+  }
   return h;
 }
 

@@ -394,6 +394,31 @@ __device__ __forceinline__ void rotor_advance(const LaunchConst& k, double dtt, 
   }
 }
 
+// The rotor of one step inside a safe horizon (run_yaw0): t's binade, and
+// with it the step's rounding dtt = (fl(t + dt) - t) - dt, is the same for
+// every step of the horizon, so the rotation by fl(omega dt) and the
+// first-order turn by omega dtt are folded once per horizon into one
+// rotation (fc, fs): 4 operations per angle instead of 7.
+template <int MOTION>
+__device__ __forceinline__ void rotor_fold(const LaunchConst& k, double dtt, double* fc, double* fs) {
+#pragma unroll
+  for (int i = 0; i < Rotor<MOTION>::NA; ++i) {
+    const double d = k.om[MOTION][i] * dtt;
+    fc[i] = fma(-k.rs[MOTION][i], d, k.rc[MOTION][i]);
+    fs[i] = fma(k.rc[MOTION][i], d, k.rs[MOTION][i]);
+  }
+}
+
+template <int MOTION>
+__device__ __forceinline__ void rotor_turn(const double* fc, const double* fs, double* rs, double* rc) {
+#pragma unroll
+  for (int i = 0; i < Rotor<MOTION>::NA; ++i) {
+    const double s0 = rs[i], c0 = rc[i];
+    rs[i] = fma(s0, fc[i], c0 * fs[i]);
+    rc[i] = fma(c0, fc[i], -(s0 * fs[i]));
+  }
+}
+
 template <bool WANT_ACC, int MOTION>
 __device__ __forceinline__ void target_from_rotor(const qt_env_params& e, const Pattern& pt, const double* rs,
                                                   const double* rc, Target& o) {
@@ -482,7 +507,7 @@ __device__ __forceinline__ void tilt_clamp(double* x, Trig& ta) {
 constexpr int kMaxHorizon = 62;
 constexpr int kVotedBurst = 4;
 
-template <bool TILT>
+template <bool TILT, bool BINADE>
 __device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizon& hz, const VelLin& lin,
                                             const Plant& pl, const double* x, double t, int rem) {
   const double tmi = hz.tmax * pl.inv_mass;
@@ -496,9 +521,17 @@ __device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizo
   h = fmin(h, (hz.pmax - fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2])))) * __builtin_amdgcn_rcp(dp));
   if (TILT) h = fmin(h, (kMaxTilt - fmax(fabs(x[6]), fabs(x[7]))) * hz.inv_dang);
   h = fmin(h, (e.max_episode_time - t) * hz.inv_tstep);
+  bool bin_ok = true;
+  if (BINADE) {
+    // t stays inside its binade [2^E, 2^(E+1)) and the binade has no tie, so
+    // every step of the horizon advances t by the same fl(t + dt) - t
+    const long long eb = __double_as_longlong(t) & 0x7ff0000000000000LL;
+    h = fmin(h, (__longlong_as_double(eb + (1LL << 52)) - t) * hz.inv_tstep);
+    bin_ok = t > 0.0 && eb != hz.tie_exp_bits;
+  }
   // rcp's error (well below 1e-6) and the step about to be voted on
   h = fma(h, 1.0 - 1e-6, -1.0);
-  const bool lane_ok = h >= 2.0 && lin.cv >= 0.0 && lin.cv <= 1.0;
+  const bool lane_ok = h >= 2.0 && lin.cv >= 0.0 && lin.cv <= 1.0 && bin_ok;
   const int hl = lane_ok ? (int)fmin(h, (double)kMaxHorizon) : 0;
   int H = 0;
 #pragma unroll
@@ -567,13 +600,20 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   // would keep their horizon at zero: their horizon leaves the tilt out and
   // every step applies the clamp.
   constexpr bool kTiltHorizon = KC != 9;
+  // The horizon's folded target rotor (rotor_fold; its horizon also ends at
+  // t's binade edge): 3 operations per angle fewer in every no-vote step, but
+  // two more live doubles per angle.  Taken where it pays in the gfx950 build:
+  // the LQI loops (LQI sinusoidal 281.5 -> 270.5 VALU per step); the 6-column
+  // loops sit at 256 architectural VGPRs and answer it with ~17 register
+  // copies per step (circular 237 -> 243), so they keep the per-step rotor.
+  constexpr bool kFold = kRotor && KC == 9;
   int s = 0;
   while (a.term == QT_TERM_RUNNING && s < nsteps) {
     const int s0 = s;
     int rem = nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0;  // steps left in this run (z stays < 1 off phase)
     RateCoef rk;
     // one closed-loop step; VOTE: end it with the stop vote (true: stop here)
-    auto step = [&](auto vote) -> bool {
+    auto step = [&](auto vote, const double* fc, const double* fs) -> bool {
       constexpr bool VOTE = decltype(vote)::value;
       rk.pin();
       const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_resid)
@@ -610,7 +650,10 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kRotor) {
-          rotor_advance<MOTION>(k, (t - t0) - e.dt, rs, rc);
+          if (VOTE || !kFold)
+            rotor_advance<MOTION>(k, (t - t0) - e.dt, rs, rc);
+          else
+            rotor_turn<MOTION>(fc, fs, rs, rc);  // the horizon's folded rotor
           target_from_rotor<FF, MOTION>(e, pt, rs, rc, tg);
         } else if constexpr (MOTION < 0) {
           rotor_target_rt<FF, true>(e, k, motion, pt, t, (t - t0) - e.dt, rs, rc, tg);
@@ -644,17 +687,26 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
     // The safe horizon's steps without the vote (in pairs: one back edge per
     // two steps), then one voted step.
     do {
-      const int H = yaw0_horizon<kTiltHorizon>(e, k.hz, lin, pl, x, t, rem);
-      for (int j = 0; j < H; j += 2) {
-        step(std::false_type{});
-        step(std::false_type{});
+      const int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
+      if constexpr (kFold) {
+        double fc[3], fs[3];  // the horizon's folded target rotor
+        rotor_fold<MOTION>(k, ((t + e.dt) - t) - e.dt, fc, fs);
+        for (int j = 0; j < H; j += 2) {
+          step(std::false_type{}, fc, fs);
+          step(std::false_type{}, fc, fs);
+        }
+      } else {
+        for (int j = 0; j < H; j += 2) {
+          step(std::false_type{}, nullptr, nullptr);
+          step(std::false_type{}, nullptr, nullptr);
+        }
       }
       rem -= H;
       // a wave with a lane near a stop (H = 0) takes a few voted steps before
       // it bounds the horizon again
       const int nv = H > 0 ? 1 : kVotedBurst;
       bool stop = false;
-      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{});
+      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{}, nullptr, nullptr);
       if (stop) break;
     } while (true);
     const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;

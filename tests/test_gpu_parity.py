@@ -222,6 +222,44 @@ def test_periodic_target_carried_trig(qt, cfg):
     assert np.isfinite(tg).all()
 
 
+@pytest.mark.parametrize("motion", ["circular", "sinusoidal", "figure8"])
+@pytest.mark.parametrize("lqi", [False, True])
+@pytest.mark.parametrize("chunks", [(3000,), (7, 993, 2000)])
+def test_carried_target_phase_after_horizons(qt, motion, lqi, chunks):
+    """The yaw-at-rest loop carries the periodic target's sin / cos across
+    steps; inside a safe horizon the LQI loops turn them by one rotor folded
+    per horizon (t's binade and with it fl(t + dt) - t fixed, the tie binade
+    excluded).  After 3,000 steps, in one launch or in chunks that start at
+    t != 0, the carried target observation equals the reference's target at
+    the final t to a few ulp: a wrong step of t's rounding in any binade would
+    show as a phase error."""
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch
+
+    env_cfg = {"target": {"motion_type": motion}}
+    ctl_cfg = {"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]} if lqi else {"dt": 0.01}
+    ctl = BatchedRiccatiLQR(ctl_cfg)
+    from quadtrack.env.config import EnvConfig
+    cfg = EnvConfig.from_dict(env_cfg)
+    env = cfg.to_params()
+    n = 256
+    seeds = np.arange(n)
+    batch = build_batch(ctl, cfg, n, seeds=seeds)
+    st = core.RolloutState.empty(n, torch.device("cuda", 0))
+    core.reset(env, batch, st)
+    for k in chunks:
+        core.rollout(env, ctl.ctrl, core.criteria(), batch, st, k)
+    torch.cuda.synchronize()
+    t = st.t.cpu().numpy()
+    assert np.all(np.abs(t - 30.0) < 1e-9)
+    tg = st.target.cpu().numpy()
+    e = O.env_params(env_cfg)
+    pat, _ = O.draws(motion, seeds)
+    ref = np.array([O.target_state(e, e.motion, pat[i], float(t[i])) for i in range(n)])
+    np.testing.assert_allclose(tg[:6].T, ref[:, :6], rtol=0, atol=2e-12)
+
+
 @pytest.mark.parametrize("lqi", [False, True])
 def test_dense_gains_yaw_at_rest(qt, lqi):
     """A full (coupled) Q gives a dense K, whose yaw-rate row is still exactly
