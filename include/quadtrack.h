@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 7
+#define QT_ABI_VERSION 8
 
 /* error codes */
 #define QT_OK 0
@@ -254,13 +254,26 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    dispatch.  batch->order must list the episodes grouped by motion: slots
    [seg_end[i-1], seg_end[i]) (seg_end[-1] = 0) all have motion seg_motion[i];
    seg_end[nseg-1] == n.  seg_motion and seg_end are HOST arrays.  The
-   yaw-at-rest fast flavour runs every group in ONE launch (each 64-lane wave
-   takes the loop specialised for its motion; the <= nseg-1 waves that straddle
-   two groups take the runtime-motion loop, same per-lane arithmetic); other
-   flavours launch once per group.  Results are identical to qt_rollout's. */
+   yaw-at-rest fast flavour runs every group in ONE launch: each group starts
+   at a 64-lane wave boundary, so every wave takes the loop specialised for its
+   motion (<= 8 non-empty groups; more fall back to one launch per group);
+   other flavours launch once per group.  Results are identical to
+   qt_rollout's. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);
+
+/* ABI 8.  One evaluation pass from reset to per-episode metrics: qt_reset
+   (offset[3][n]), then qt_rollout (nsteps, no recording), then
+   qt_episode_metrics into met[QT_MET_ROWS][n], with the same results bit for
+   bit, in one launch set: the rollout kernel forms the reset state in its
+   prologue instead of loading it and writes the metrics rows in its epilogue.
+   st receives the state qt_rollout leaves.  nseg > 0: a motion-grouped batch
+   as qt_rollout_grouped (seg_motion, seg_end HOST arrays); nseg == 0: as
+   qt_rollout. */
+int qt_rollout_fresh(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                     const qt_batch* batch, const double* offset, qt_state st, int32_t nsteps, double* met,
+                     int32_t nseg, const int32_t* seg_motion, const int64_t* seg_end, void* stream);
 
 /* Open-loop QuadcopterEnv.step(action) for a batch (quadcopter_env.py:152-293):
    action[4][n] (NaN/Inf zeroed, thrust and rate clipping), RK4/Euler, state

@@ -560,6 +560,11 @@ struct LaunchConst {
   // qt_rollout_rewards (exact step only): [2][n] reward sum and last
   // post-step tracking error, accumulated across launches; null otherwise
   double* reward;
+  // qt_rollout_fresh: the reset offsets[3][n] (the kernel forms the reset
+  // state instead of loading one; null: load) and the metrics rows
+  // met[QT_MET_ROWS][n] written at the end (null: none)
+  const double* fresh_off;
+  double* met;
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)

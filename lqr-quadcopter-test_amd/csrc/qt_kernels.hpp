@@ -174,6 +174,47 @@ __device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<
   }
 }
 
+// compute_episode_metrics (utils/metrics.py:264-338) of one episode from its
+// accumulators and env time (the Evaluator's record, eval.py:142-159) into
+// met[QT_MET_ROWS][n] column e: metrics_kernel, and the rollout epilogue of a
+// fresh pass (qt_rollout_fresh).
+__device__ __forceinline__ void store_metrics(const qt_criteria& cr, Acc a, double t, double* met, int64_t n,
+                                              int64_t e) {
+  double m[QT_MET_ROWS];
+  if (a.steps == 0) {
+#pragma unroll
+    for (int i = 0; i < QT_MET_ROWS; ++i) m[i] = 0.0;
+  } else {
+    // an overshoot still open at the end counts if long enough (metrics.py:256-259)
+    if (a.os_streak >= cr.overshoot_window) {
+      a.os_count += 1;
+      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
+    }
+    if (a.steps < cr.overshoot_window) {  // metrics.py:225-226
+      a.os_count = 0;
+      a.os_max = 0.0;
+    }
+    const double ns = a.steps;
+    const double ratio = a.on_pre / ns;
+    m[QT_MET_DURATION] = t;
+    m[QT_MET_ON_TARGET_RATIO] = ratio;
+    m[QT_MET_MEAN_ERR] = a.sum_e / ns;
+    m[QT_MET_MAX_ERR] = a.max_e;
+    m[QT_MET_RMS_ERR] = sqrt(a.sum_e2 / ns);
+    m[QT_MET_TOTAL_EFFORT] = a.sum_u;
+    m[QT_MET_MEAN_EFFORT] = a.sum_u / ns;
+    m[QT_MET_OS_COUNT] = a.os_count;
+    m[QT_MET_OS_MAX] = a.os_max;
+    m[QT_MET_SUCCESS] = (t >= cr.min_episode_duration && ratio >= cr.min_on_target_ratio) ? 1.0 : 0.0;
+    m[QT_MET_TERM] = a.term;
+    m[QT_MET_VIOLATIONS] = a.viol;
+    m[QT_MET_ENV_ON_TARGET_RATIO] = a.on_post / ns;
+    m[QT_MET_STEPS] = ns;
+  }
+#pragma unroll
+  for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
+}
+
 // Overshoot state machine of detect_overshoots (utils/metrics.py:205-261),
 // streamed over the pre-step errors: called for every step k >= 1 with the
 // on-target flag of step k (the flag of k-1 is a.prev_on).  os_streak is the
@@ -732,7 +773,11 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // UNI (fast flavours): no per-episode mass, hover thrust or gains — the
 // plant constants come from the launch (LaunchConst) and the gains from
 // uniform addresses, all in SGPRs (checked on the host, launch_rollout).
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
+// FRESH: the fresh-pass prologue / epilogue (LaunchConst::fresh_off, met) is
+// compiled in (the grouped kernel leaves it out: its two-waves-per-SIMD
+// register budget has no room, and its fresh passes take qt_reset and
+// metrics_kernel around the launch).
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true>
 __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                              const BatchDev& b, const qt_state& st, int nsteps,
                                              double* __restrict__ rec, int deferred, const LaunchConst& lc,
@@ -749,19 +794,49 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   // integ: LQI integral (KC 9) | PID integral error + last observation time (KC 3)
   constexpr int NI = KC == 9 ? 3 : (KC == 3 ? 4 : 0);
   double x[12], integ[4] = {0, 0, 0, 0};  // PID: row 3 (last observation time) is loaded
-#pragma unroll
-  for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) integ[i] = st.integ[i * n + ep];
   Target tg;
+  double t;
+  Acc a;
+  if (FRESH && lc.fresh_off) {
+    // a fresh pass (qt_rollout_fresh): the state qt_reset would store
+    // (reset_kernel, quadcopter_env.py:111-150; fresh controller,
+    // riccati_lqr.py:1073-1086), formed here instead of loaded
+    target_state<true>(e, motion, pt, 0.0, tg);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    tg.p[i] = st.target[i * n + ep];
-    tg.v[i] = st.target[(3 + i) * n + ep];
-    tg.a[i] = st.target[(6 + i) * n + ep];
+    for (int i = 0; i < 3; ++i) x[i] = tg.p[i] + lc.fresh_off[i * n + ep];
+#pragma unroll
+    for (int i = 3; i < 12; ++i) x[i] = 0.0;
+    if (KC == 3) integ[3] = __longlong_as_double(0x7ff8000000000000LL);  // PID: no previous observation time (NaN)
+    t = 0.0;
+    a = Acc{0, 0, -INFINITY, 0, 0, 0, 0, 0, 0, -1, -1, 0, 0, QT_TERM_RUNNING};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) x[i] = st.x[i * n + ep];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) integ[i] = st.integ[i * n + ep];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      tg.p[i] = st.target[i * n + ep];
+      tg.v[i] = st.target[(3 + i) * n + ep];
+      tg.a[i] = st.target[(6 + i) * n + ep];
+    }
+    t = st.t[ep];
+    a = load_acc(st.acc, n, ep);
   }
-  double t = st.t[ep];
-  Acc a = load_acc(st.acc, n, ep);
+  auto store_state = [&]() {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      st.target[i * n + ep] = tg.p[i];
+      st.target[(3 + i) * n + ep] = tg.v[i];
+      st.target[(6 + i) * n + ep] = tg.a[i];
+    }
+    st.t[ep] = t;
+    store_acc(st.acc, n, ep, a);
+  };
 
   // Which step the wavefront runs (uniform).  A fast flavour is launched only
   // when the launch-level preconditions hold (fast_path_ok, no recording); it
@@ -786,6 +861,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   if (FLAVOR != kExact) {
     if (!wave_ok) {
       if (lc.defer_flag) *lc.defer_flag = lc.epoch;  // the exact pass has work (every lane stores the same value)
+      if (FRESH && lc.fresh_off) store_state();  // the reset state, for the exact pass (launched without fresh_off)
       return;
     }
 #if QT_CLOCK_STAMP && defined(QT_FAST_TU)
@@ -822,18 +898,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     for (int i = 0; i < 3; ++i) tg.a[i] = full.a[i];
   }
 
-#pragma unroll
-  for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    st.target[i * n + ep] = tg.p[i];
-    st.target[(3 + i) * n + ep] = tg.v[i];
-    st.target[(6 + i) * n + ep] = tg.a[i];
-  }
-  st.t[ep] = t;
-  store_acc(st.acc, n, ep, a);
+  store_state();
+  if (FRESH && lc.met) store_metrics(cr, a, t, lc.met, n, ep);  // a fresh pass: the metrics rows (metrics_kernel)
 }
 
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
@@ -870,19 +936,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
   if (slot < 0) return;
   switch (wave_motion(b, p)) {
     case QT_MOTION_STATIONARY:
-      rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
     case QT_MOTION_LINEAR:
-      rollout_lane<kYaw0, QT_MOTION_LINEAR, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_LINEAR, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
     case QT_MOTION_CIRCULAR:
-      rollout_lane<kYaw0, QT_MOTION_CIRCULAR, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_CIRCULAR, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
     case QT_MOTION_SINUSOIDAL:
-      rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
     default:
-      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
   }
 }
 

@@ -164,40 +164,7 @@ __global__ __launch_bounds__(kBlock) void metrics_kernel(qt_criteria cr, int64_t
                                                          const double* __restrict__ t, double* met) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  Acc a = load_acc(acc, n, e);
-  double m[QT_MET_ROWS];
-  if (a.steps == 0) {
-#pragma unroll
-    for (int i = 0; i < QT_MET_ROWS; ++i) m[i] = 0.0;
-  } else {
-    // an overshoot still open at the end counts if long enough (metrics.py:256-259)
-    if (a.os_streak >= cr.overshoot_window) {
-      a.os_count += 1;
-      if (a.os_cur > a.os_max) a.os_max = a.os_cur;
-    }
-    if (a.steps < cr.overshoot_window) {  // metrics.py:225-226
-      a.os_count = 0;
-      a.os_max = 0.0;
-    }
-    const double ns = a.steps;
-    const double ratio = a.on_pre / ns;
-    m[QT_MET_DURATION] = t[e];
-    m[QT_MET_ON_TARGET_RATIO] = ratio;
-    m[QT_MET_MEAN_ERR] = a.sum_e / ns;
-    m[QT_MET_MAX_ERR] = a.max_e;
-    m[QT_MET_RMS_ERR] = sqrt(a.sum_e2 / ns);
-    m[QT_MET_TOTAL_EFFORT] = a.sum_u;
-    m[QT_MET_MEAN_EFFORT] = a.sum_u / ns;
-    m[QT_MET_OS_COUNT] = a.os_count;
-    m[QT_MET_OS_MAX] = a.os_max;
-    m[QT_MET_SUCCESS] = (t[e] >= cr.min_episode_duration && ratio >= cr.min_on_target_ratio) ? 1.0 : 0.0;
-    m[QT_MET_TERM] = a.term;
-    m[QT_MET_VIOLATIONS] = a.viol;
-    m[QT_MET_ENV_ON_TARGET_RATIO] = a.on_post / ns;
-    m[QT_MET_STEPS] = ns;
-  }
-#pragma unroll
-  for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
+  store_metrics(cr, load_acc(acc, n, e), t[e], met, n, e);
 }
 
 // numpy's summation order (np.add.reduce of a contiguous float64 vector; see
@@ -629,10 +596,12 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 // pass with runtime motion over the same slot mapping.
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
-                   double* rec, bool grouped = false, double* reward = nullptr) {
+                   double* rec, bool grouped = false, double* reward = nullptr, const double* fresh_off = nullptr,
+                   double* met = nullptr) {
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   lc.hz = make_horizon(e, c, lc.rl);       // the yaw-at-rest loop's safe horizon
   lc.reward = reward;
+  lc.fresh_off = fresh_off, lc.met = met;  // qt_rollout_fresh: reset in the prologue, metrics in the epilogue
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
   // rewards are accumulated by the exact step only
@@ -642,10 +611,68 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
     lc.epoch = g_defer_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
     launch_fast(flavor, uni, grouped, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
+    lc.fresh_off = nullptr;  // the fast kernel stored the reset state of the waves it left
   }
   dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, grouped ? -1 : motion, flavor, grid, s, e, c, cr, b, st, nsteps, rec,
                                 lc);
   return check_launch();
+}
+
+// qt_rollout / qt_rollout_grouped / qt_rollout_fresh after validation:
+// nseg == 0, one launch set over the batch; else motion groups (wave-aligned
+// segments in one yaw-at-rest launch, or one launch set per group).
+// fresh_off / met: a fresh pass (reset in the prologue, metrics rows in the
+// epilogue).
+int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const qt_batch* batch,
+                  qt_state st, int nsteps, double* rec, int32_t nseg, const int32_t* seg_motion,
+                  const int64_t* seg_end, hipStream_t s, const double* fresh_off = nullptr, double* met = nullptr) {
+  BatchDev b = to_dev(batch);
+  const bool ff = c.feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
+  const bool ks = batch->k_structured != 0;
+  const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
+  if (nseg == 0)
+    return launch_rollout(batch->k_cols, ff, ks, no_yaw, batch->motion ? -1 : e.motion, grid_of(batch->n), s, e, c,
+                          cr, b, st, nsteps, rec, false, nullptr, fresh_off, met);
+  if (flavor_for(batch->k_cols, ks, no_yaw, e, c, rec) == kYaw0) {
+    // every group in one launch, each starting at a wavefront boundary (BatchDev's
+    // wave-aligned segments; both the fast kernel and its exact pass map slots so)
+    BatchDev bg = b;
+    int64_t waves = 0, prev_end = 0;
+    bool fits = true;
+    for (int32_t i = 0; i < nseg && fits; ++i) {
+      const int64_t cnt = seg_end[i] - prev_end;
+      prev_end = seg_end[i];
+      if (cnt == 0) continue;
+      if (bg.nseg == 8) {
+        fits = false;
+        break;
+      }
+      waves += (cnt + 63) / 64;
+      bg.seg_motion[bg.nseg] = (int8_t)seg_motion[i];
+      bg.seg_end[bg.nseg] = seg_end[i];
+      bg.wave_end[bg.nseg] = waves;
+      ++bg.nseg;
+    }
+    if (fits) {
+      // the grouped kernel has no fresh prologue / epilogue (rollout_lane's FRESH)
+      if (fresh_off) reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(e, b, fresh_off, st);
+      const int rc = launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, (int)((waves * 64 + kBlock - 1) / kBlock), s,
+                                    e, c, cr, bg, st, nsteps, rec, true);
+      if (rc != QT_OK || !met) return rc;
+      metrics_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(cr, batch->n, st.acc, st.t, met);
+      return check_launch();
+    }
+  }
+  for (int32_t i = 0; i < nseg; ++i) {
+    b.slot0 = i ? seg_end[i - 1] : 0;
+    b.slot_end = seg_end[i];
+    if (b.slot_end == b.slot0) continue;
+    const int grid = grid_of(b.slot_end - b.slot0);
+    if (launch_rollout(batch->k_cols, ff, ks, no_yaw, seg_motion[i], grid, s, e, c, cr, b, st, nsteps, rec,
+                       false, nullptr, fresh_off, met) != QT_OK)
+      return QT_ELAUNCH;
+  }
+  return QT_OK;
 }
 
 }  // namespace
@@ -692,14 +719,7 @@ int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_cr
   if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
   if (batch->n == 0 || nsteps == 0) return QT_OK;  // nothing to run: no per-episode pointer is read
   if (!valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
-  const BatchDev b = to_dev(batch);
-  const int grid = grid_of(batch->n);
-  const int motion = batch->motion ? -1 : env->motion;
-  hipStream_t s = (hipStream_t)stream;
-  const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
-  const bool ks = batch->k_structured != 0;
-  const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
-  return launch_rollout(batch->k_cols, ff, ks, no_yaw, motion, grid, s, *env, *ctrl, *crit, b, st, nsteps, rec);
+  return rollout_batch(*env, *ctrl, *crit, batch, st, nsteps, rec, 0, nullptr, nullptr, (hipStream_t)stream);
 }
 
 int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
@@ -729,45 +749,30 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
   }
   if (prev != batch->n) return QT_EINVAL;
   if (batch->n == 0 || nsteps == 0) return QT_OK;
-  BatchDev b = to_dev(batch);
-  hipStream_t s = (hipStream_t)stream;
-  const bool ff = ctrl->feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
-  const bool ks = batch->k_structured != 0;
-  const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
-  if (flavor_for(batch->k_cols, ks, no_yaw, *env, *ctrl, rec) == kYaw0) {
-    // every group in one launch, each starting at a wavefront boundary (BatchDev's
-    // wave-aligned segments; both the fast kernel and its exact pass map slots so)
-    BatchDev bg = b;
-    int64_t waves = 0, prev_end = 0;
-    bool fits = true;
-    for (int32_t i = 0; i < nseg && fits; ++i) {
-      const int64_t cnt = seg_end[i] - prev_end;
-      prev_end = seg_end[i];
-      if (cnt == 0) continue;
-      if (bg.nseg == 8) {
-        fits = false;
-        break;
-      }
-      waves += (cnt + 63) / 64;
-      bg.seg_motion[bg.nseg] = (int8_t)seg_motion[i];
-      bg.seg_end[bg.nseg] = seg_end[i];
-      bg.wave_end[bg.nseg] = waves;
-      ++bg.nseg;
-    }
-    if (fits)
-      return launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, (int)((waves * 64 + kBlock - 1) / kBlock), s, *env,
-                            *ctrl, *crit, bg, st, nsteps, rec, true);
-  }
+  return rollout_batch(*env, *ctrl, *crit, batch, st, nsteps, rec, nseg, seg_motion, seg_end, (hipStream_t)stream);
+}
+
+int qt_rollout_fresh(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
+                     const qt_batch* batch, const double* offset, qt_state st, int32_t nsteps, double* met, int32_t nseg,
+                     const int32_t* seg_motion, const int64_t* seg_end, void* stream) {
+  if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
+  if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
+  if (batch->n == 0) return QT_OK;  // empty: no per-episode pointer is read
+  if (!offset || !met || !valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
+  if (nseg < 0 || (nseg > 0 && (!seg_motion || !seg_end))) return QT_EINVAL;
+  int64_t prev = 0;
   for (int32_t i = 0; i < nseg; ++i) {
-    b.slot0 = i ? seg_end[i - 1] : 0;
-    b.slot_end = seg_end[i];
-    if (b.slot_end == b.slot0) continue;
-    const int grid = grid_of(b.slot_end - b.slot0);
-    if (launch_rollout(batch->k_cols, ff, ks, no_yaw, seg_motion[i], grid, s, *env, *ctrl, *crit, b, st, nsteps,
-                       rec) != QT_OK)
-      return QT_ELAUNCH;
+    if (seg_end[i] < prev || seg_end[i] > batch->n || seg_motion[i] < 0 || seg_motion[i] > 4) return QT_EINVAL;
+    prev = seg_end[i];
   }
-  return QT_OK;
+  if (nseg > 0 && prev != batch->n) return QT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (nsteps == 0) {  // nothing to run: the reset and the metrics of the reset state
+    reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(*env, to_dev(batch), offset, st);
+    metrics_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(*crit, batch->n, st.acc, st.t, met);
+    return check_launch();
+  }
+  return rollout_batch(*env, *ctrl, *crit, batch, st, nsteps, nullptr, nseg, seg_motion, seg_end, s, offset, met);
 }
 
 int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action, qt_state st, double* err,

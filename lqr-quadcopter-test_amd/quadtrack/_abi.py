@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
 LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # enums (include/quadtrack.h)
 MOTIONS = ("stationary", "linear", "circular", "sinusoidal", "figure8")
@@ -79,7 +79,7 @@ class State(C.Structure):
                 ("target", C.c_void_p)]
 
 
-EXPORTS = ("qt_abi_version", "qt_host_alloc", "qt_host_free", "qt_stream_sync", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_rewards", "qt_rollout_grouped",
+EXPORTS = ("qt_abi_version", "qt_host_alloc", "qt_host_free", "qt_stream_sync", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_rewards", "qt_rollout_grouped", "qt_rollout_fresh",
            "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary",
            "qt_summary_parts", "qt_summary_numpy", "qt_stream_uniform")
@@ -111,6 +111,8 @@ def load():
     L.qt_rollout_rewards.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, vp]
     L.qt_rollout_grouped.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, i32,
                                      P(C.c_int32), P(C.c_int64), vp]
+    L.qt_rollout_fresh.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), vp, State, i32, vp, i32,
+                                   P(C.c_int32), P(C.c_int64), vp]
     L.qt_seed_uniform.argtypes = [i64, vp, i32, vp, vp, vp, vp]
     L.qt_env_step.argtypes = [P(EnvParams), P(Batch), vp, State, vp, vp, vp, vp, vp, vp]
     L.qt_compute_action.argtypes = [P(CtrlParams), P(Batch), vp, vp, vp, vp, vp, vp]

@@ -311,6 +311,31 @@ def rollout(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatc
                                  int(nsteps), ptr(rec), stream_of(batch.device)), "qt_rollout")
 
 
+def rollout_fresh(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState,
+                  nsteps: int, met: torch.Tensor | None = None) -> torch.Tensor:
+    """reset -> rollout(nsteps) -> episode_metrics as one launch set
+    (qt_rollout_fresh, ABI 8): the rollout kernel forms the reset state from
+    batch.offset in its prologue and writes the metrics rows in its epilogue.
+    Same results as the three calls, bit for bit.  Returns met [MET_ROWS, n]."""
+    lib = _abi.load()
+    n = batch.n
+    if met is None:
+        met = torch.empty(MET_ROWS, n, dtype=F64, device=batch.device)
+    elif met.dtype != F64 or not met.is_contiguous() or tuple(met.shape) != (MET_ROWS, n):
+        raise ValueError("met must be a contiguous float64 [MET_ROWS, n] tensor")
+    nseg, sm, se = 0, None, None
+    if batch.groups is not None:
+        seg_motion, seg_end = batch.groups
+        nseg = len(seg_motion)
+        sm = (C.c_int32 * nseg)(*[int(v) for v in seg_motion])
+        se = (C.c_int64 * nseg)(*[int(v) for v in seg_end])
+    with torch.cuda.device(batch.device):
+        check(lib.qt_rollout_fresh(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()),
+                                   ptr(batch.offset), st.c_state(), int(nsteps), ptr(met), nseg, sm, se,
+                                   stream_of(batch.device)), "qt_rollout_fresh")
+    return met
+
+
 def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState,
                     nsteps: int, reward: torch.Tensor):
     """qt_rollout_rewards: the exact-step rollout that also accumulates

@@ -282,16 +282,20 @@ def run_closed_loop(controller: BatchedRiccatiLQR, env_config=None, n: int | Non
     run, perm = batch.physical_groups() if batch.groups is not None and batch.order is not None else (batch, None)
     st = core.RolloutState.empty(n, batch.device)
     core.validate(run, st)
-    core.reset(env, run, st)
     total = max_steps if max_steps is not None else max_steps_for(env)
     step = chunk or total
     rec = torch.full((total, 16, n), float("nan"), dtype=F64, device=batch.device) if record else None
-    done = 0
-    while done < total:
-        k = min(step, total - done)
-        core.rollout(env, controller.ctrl, crit, run, st, k, None if rec is None else rec[done:done + k])
-        done += k
-    met = core.episode_metrics(crit, st)
+    if rec is None and step >= total:
+        # one launch set: reset in the rollout's prologue, metrics in its epilogue
+        met = core.rollout_fresh(env, controller.ctrl, crit, run, st, total)
+    else:
+        core.reset(env, run, st)
+        done = 0
+        while done < total:
+            k = min(step, total - done)
+            core.rollout(env, controller.ctrl, crit, run, st, k, None if rec is None else rec[done:done + k])
+            done += k
+        met = core.episode_metrics(crit, st)
     if perm is not None:
         met = core.unpermute(met, perm)
         st = core.RolloutState(x=core.unpermute(st.x, perm), integ=core.unpermute(st.integ, perm),
