@@ -565,6 +565,11 @@ struct LaunchConst {
   // met[QT_MET_ROWS][n] written at the end (null: none)
   const double* fresh_off;
   double* met;
+  // the fused summary of a fresh pass (exact-pass launch, summary_tail):
+  // out[11], work[grid][11], the per-stream workgroup counter; null: none
+  double* sum_out;
+  double* sum_work;
+  unsigned* sum_count;
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)
