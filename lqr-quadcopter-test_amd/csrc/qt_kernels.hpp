@@ -830,7 +830,14 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
           step(std::false_type{}, fc, fs);
         }
       } else {
-        for (int j = 0; j < H; j += 2) {
+        // four steps per back edge, then the horizon's last two (H is even)
+        for (int j = 4; j <= H; j += 4) {
+          step(std::false_type{}, nullptr, nullptr);
+          step(std::false_type{}, nullptr, nullptr);
+          step(std::false_type{}, nullptr, nullptr);
+          step(std::false_type{}, nullptr, nullptr);
+        }
+        if (H & 2) {
           step(std::false_type{}, nullptr, nullptr);
           step(std::false_type{}, nullptr, nullptr);
         }
