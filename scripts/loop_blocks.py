@@ -8,7 +8,7 @@ common path has no taken branch but the loop back-edge.
 
 --table lists, for every yaw-at-rest rollout_kernel instance and every
 per-motion loop of rollout_grouped_kernel, the instructions one wave issues
-per env step inside the safe horizon (the two-step no-vote loop, halved) and
+per env step inside the safe horizon (the no-vote loop over its 4 or 2 steps) and
 in the voted step that ends each horizon (run_yaw0).
 """
 
@@ -54,8 +54,12 @@ def step_loops(blocks):
 
 
 def row(tag, motion, pair, voted):
+    """The no-vote loop runs four steps per back edge (two in the LQI loops
+    with the folded target rotor): told apart by its size against the voted
+    step's."""
     v = f"{voted['n']:5d} {voted['valu']:5d} {voted['salu']:5d}" if voted else "    -     -     -"
-    print(f"{tag:46s} {motion:11s} {pair['n'] / 2:6.1f} {pair['valu'] / 2:6.1f} {pair['salu'] / 2:5.1f}   {v}")
+    k = 4 if voted and pair["n"] > 2.5 * voted["n"] else 2
+    print(f"{tag:46s} {motion:11s} {pair['n'] / k:6.1f} {pair['valu'] / k:6.1f} {pair['salu'] / k:5.1f}   {v}")
 
 
 def table(s):
