@@ -154,7 +154,12 @@ __device__ __forceinline__ void figure8_recip(const qt_env_params& e, double om,
   const double den = 1.0 + st * st;
   const double dcos = -st * om, dsin = ct * om;
   const double dden = 2.0 * st * dsin;
-  const double r = 1.0 / den, r2 = r * r;
+  // 1 / den for den in [1, 2]: v_rcp_f64's estimate and two Newton steps
+  // (within an ulp; the division's scale / fixup steps are not needed there)
+  double r = __builtin_amdgcn_rcp(den);
+  r = fma(r, fma(-den, r, 1.0), r);
+  r = fma(r, fma(-den, r, 1.0), r);
+  const double r2 = r * r;
   o.p[0] = e.center[0] + sc * ct * r;
   o.p[1] = e.center[1] + sc * st * ct * r;
   o.p[2] = e.center[2];
@@ -168,8 +173,8 @@ __device__ __forceinline__ void figure8_recip(const qt_env_params& e, double om,
 // acceleration clamp (403-405).  WANT_ACC = false skips the acceleration,
 // which only the feed-forward path reads (riccati_lqr.py:853-861).
 // RECIP (fast step, no acceleration wanted): the figure-8's four divisions
-// by den and den^2 become one correctly rounded reciprocal and products
-// (<= 2 ulp per component; without feed-forward no forward difference reads
+// by den and den^2 become one reciprocal (within an ulp) and products
+// (<= 3 ulp per component; without feed-forward no forward difference reads
 // them).
 template <bool WANT_ACC, bool RECIP = false>
 __device__ __forceinline__ void target_state(const qt_env_params& e, int motion, const Pattern& pt, double t,
