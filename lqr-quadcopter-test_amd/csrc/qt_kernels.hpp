@@ -844,8 +844,9 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       }
       rem -= H;
       // a wave with a lane near a stop (H = 0) takes a few voted steps before
-      // it bounds the horizon again
-      const int nv = H > 0 ? 1 : kVotedBurst;
+      // it bounds the horizon again; without a horizon (hz.on == 0: a
+      // non-finite limit) every step is voted
+      const int nv = H > 0 ? 1 : (k.hz.on ? kVotedBurst : (1 << 30));
       bool stop = false;
       for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{}, nullptr, nullptr);
       if (stop) break;

@@ -339,7 +339,8 @@ def test_chunked_equals_single_launch(qt, motion):
 
 
 @pytest.mark.parametrize("case", ["linear_lqr", "sinusoidal_lqi", "figure8_ff", "mixed_mass", "circular_tight",
-                                  "pid_integral", "pid_ff_circular", "lqr_heuristic_ff"])
+                                  "pid_integral", "pid_ff_circular", "lqr_heuristic_ff", "speed_clamp",
+                                  "odd_episode_time", "mass_spread_lqi", "no_limits"])
 def test_fast_path_equals_exact_path(qt, case):
     """The branch-light fast step (taken when the wave qualifies and nothing is
     recorded) against the exact step (forced by recording): the same decisions
@@ -373,6 +374,18 @@ def test_fast_path_equals_exact_path(qt, case):
         kind, env = "pid", {"target": {"motion_type": "circular", "speed": 3.0}}
         ctl_cfg = {"feedforward_enabled": True, "ff_velocity_gain": [0.3, 0.3, 0.1], "ff_acceleration_gain": 0.2,
                    "ki_pos": 0.01, "integral_limit": 0.5, "ff_max_velocity": 2.5}
+    elif case == "speed_clamp":  # the safe horizon near the velocity clamp: a 2.9 m/s target, 3 m/s clamp
+        env = {"target": {"motion_type": "linear", "speed": 2.9}, "simulation": {"max_velocity": 3.0}}
+        ctl_cfg.update(q_pos=[1.0, 1.0, 40.0], q_vel=[0.01, 0.01, 4.0])
+    elif case == "odd_episode_time":  # the horizon's time bound ends mid-horizon-grid
+        env = {"target": {"motion_type": "circular"}, "simulation": {"max_episode_time": 7.013}}
+    elif case == "no_limits":  # infinite speed / position limits: no safe horizon, every step voted
+        env = {"target": {"motion_type": "circular"},
+               "simulation": {"max_velocity": float("inf"), "max_position": float("inf")}}
+    elif case == "mass_spread_lqi":  # per-lane speed / position bounds from per-episode masses
+        env = {"target": {"motion_type": "sinusoidal"}}
+        ctl_cfg.update(use_lqi=True, q_int=[1e-3, 1e-3, 1e-2])
+        kw = dict(plant_mass=0.3 + 2.7 * np.arange(n) / n)
     else:
         kind, env = "lqr", {"target": {"motion_type": "figure8"}}
         ctl_cfg = {"q_pos": [2e-4, 3e-4, 20.0], "feedforward_enabled": True, "ff_velocity_gain": 0.2,
