@@ -206,7 +206,9 @@ def main():
             # RCCL's own stream after this pass's partials and overlaps the next
             # pass's rollout instead of serialising ~tens of us of collective
             # latency into every pass; all are waited for before the clock stops.
-            pending.append(dist.all_reduce(part[0:5], async_op=True))
+            # (the partials tensor is held until the collective is waited for, so the
+            # allocator cannot hand its memory to a later pass while RCCL reads it)
+            pending.append((dist.all_reduce(part[0:5], async_op=True), part))
         return met
 
     # warm-up: --warmup passes, then chunks of ~0.1 s until --warmup-seconds
@@ -233,7 +235,7 @@ def main():
         torch.cuda.synchronize()
         warm += chunk
         chunk = max(1, min(1000, int(0.1 / max((time.perf_counter() - tc) / chunk, 1e-6))))
-    for w in pending:
+    for w, _ in pending:
         w.wait()
     pending.clear()
     if world > 1:
@@ -243,7 +245,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         met = one_pass(True)
-    for w in pending:
+    for w, _ in pending:
         w.wait()
     pending.clear()
     torch.cuda.synchronize()
