@@ -195,12 +195,12 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        # reset -> rollout -> per-episode metrics -> summary partials as one launch set
-        # (qt_rollout_fresh: the summary reduced inside the exact-pass launch)
-        met, part = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps, summary=True)
+        # reset -> rollout -> per-episode metrics as one launch set (qt_rollout_fresh)
+        met = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps)
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
+        part = core.summary_partials(met)
         if world > 1:
             # RCCL over xGMI: the one data exchange.  async_op: it runs on
             # RCCL's own stream after this pass's partials and overlaps the next

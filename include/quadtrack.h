@@ -270,17 +270,10 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    prologue instead of loading it and writes the metrics rows in its epilogue.
    st receives the state qt_rollout leaves.  nseg > 0: a motion-grouped batch
    as qt_rollout_grouped (seg_motion, seg_end HOST arrays); nseg == 0: as
-   qt_rollout.  summary != NULL: also the EvaluationSummary partials of met
-   (qt_summary_parts' 11 values, mu_ratio = mu_err = 0, one part per 256
-   episodes: bit for bit qt_summary_parts with nparts = n / 256 when 256
-   divides n) into summary[11], with summary_work holding ceil(n / 256) * 11
-   doubles; for a batch without `order` and groups they are reduced inside the
-   exact-pass launch (each workgroup its own episodes, the last one folding),
-   otherwise by qt_summary_parts' kernels after it, in the same order. */
+   qt_rollout. */
 int qt_rollout_fresh(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                      const qt_batch* batch, const double* offset, qt_state st, int32_t nsteps, double* met,
-                     double* summary, double* summary_work, int32_t nseg, const int32_t* seg_motion,
-                     const int64_t* seg_end, void* stream);
+                     int32_t nseg, const int32_t* seg_motion, const int64_t* seg_end, void* stream);
 
 /* Open-loop QuadcopterEnv.step(action) for a batch (quadcopter_env.py:152-293):
    action[4][n] (NaN/Inf zeroed, thrust and rate clipping), RK4/Euler, state

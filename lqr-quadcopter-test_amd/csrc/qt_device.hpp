@@ -147,7 +147,7 @@ __device__ __forceinline__ int periodic_angles(int motion, const Pattern& pt, do
 
 // Figure-8 position / velocity (target_motion.py:173-204) from sin / cos of
 // theta = omega t, without the acceleration: the four divisions by den and
-// den^2 as one correctly rounded reciprocal and products (<= 2 ulp per
+// den^2 as one reciprocal (within an ulp) and products (<= 3 ulp per
 // component; without feed-forward no forward difference reads them).
 __device__ __forceinline__ void figure8_recip(const qt_env_params& e, double om, double st, double ct, Target& o) {
   const double sc = e.amplitude;
@@ -570,11 +570,6 @@ struct LaunchConst {
   // met[QT_MET_ROWS][n] written at the end (null: none)
   const double* fresh_off;
   double* met;
-  // the fused summary of a fresh pass (exact-pass launch, summary_tail):
-  // out[11], work[grid][11], the per-stream workgroup counter; null: none
-  double* sum_out;
-  double* sum_work;
-  unsigned* sum_count;
 };
 
 // omega of the periodic patterns' angles (make_pattern; target_motion.py:78, 135, 171)

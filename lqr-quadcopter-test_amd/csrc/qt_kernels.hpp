@@ -174,99 +174,6 @@ __device__ __forceinline__ void load_gains(const BatchDev& b, int64_t ep, Gains<
   }
 }
 
-// EvaluationSummary partials (utils/metrics.py:341-390): fixed summation
-// order (bitwise reproducible for a given n), first-index argmax/argmin.
-// Partial vector: [7 sums, max, argmax, min, argmin]; an argmax/argmin < 0
-// marks an empty partial.
-constexpr int kSumBlock = 256;
-constexpr int kSumParts = 11;
-
-struct SumPart {
-  double s[7];
-  double vmax, vmin;
-  int64_t imax, imin;
-};
-
-__device__ __forceinline__ void sum_empty(SumPart& p) {
-#pragma unroll
-  for (int k = 0; k < 7; ++k) p.s[k] = 0.0;
-  p.vmax = -INFINITY, p.vmin = INFINITY, p.imax = -1, p.imin = -1;
-}
-
-// episodes [lo, hi) of met, strided over the block's threads
-__device__ __forceinline__ void sum_accumulate(SumPart& p, int64_t n, const double* __restrict__ met, double mu_r,
-                                               double mu_e, int64_t lo, int64_t hi) {
-  for (int64_t e = lo + threadIdx.x; e < hi; e += kSumBlock) {
-    const double r = met[QT_MET_ON_TARGET_RATIO * n + e], er = met[QT_MET_MEAN_ERR * n + e];
-    p.s[0] += r;
-    p.s[1] += er;
-    p.s[2] += met[QT_MET_MEAN_EFFORT * n + e];
-    p.s[3] += met[QT_MET_SUCCESS * n + e];
-    p.s[4] += 1.0;
-    p.s[5] += (r - mu_r) * (r - mu_r);
-    p.s[6] += (er - mu_e) * (er - mu_e);
-    if (r > p.vmax || p.imax < 0) p.vmax = r, p.imax = e;
-    if (r < p.vmin || p.imin < 0) p.vmin = r, p.imin = e;
-  }
-}
-
-// tree-combine every thread's partial (fixed pairing); thread 0 writes out[11]
-__device__ inline void sum_block_reduce(const SumPart& p, double* out) {
-  __shared__ double sh[7][kSumBlock];
-  __shared__ double shx[2][kSumBlock];
-  __shared__ int64_t shi[2][kSumBlock];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] = p.s[k];
-  shx[0][threadIdx.x] = p.vmax;
-  shx[1][threadIdx.x] = p.vmin;
-  shi[0][threadIdx.x] = p.imax;
-  shi[1][threadIdx.x] = p.imin;
-  __syncthreads();
-  for (int w = kSumBlock / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      const int o = threadIdx.x + w;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] += sh[k][o];
-      // keep the lowest index among equal values (np.argmax/argmin first occurrence)
-      const int64_t ia = shi[0][threadIdx.x], ib = shi[0][o];
-      if (ib >= 0 && (ia < 0 || shx[0][o] > shx[0][threadIdx.x] ||
-                      (shx[0][o] == shx[0][threadIdx.x] && ib < ia)))
-        shx[0][threadIdx.x] = shx[0][o], shi[0][threadIdx.x] = ib;
-      const int64_t ja = shi[1][threadIdx.x], jb = shi[1][o];
-      if (jb >= 0 && (ja < 0 || shx[1][o] < shx[1][threadIdx.x] ||
-                      (shx[1][o] == shx[1][threadIdx.x] && jb < ja)))
-        shx[1][threadIdx.x] = shx[1][o], shi[1][threadIdx.x] = jb;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) out[k] = sh[k][0];
-    out[7] = shx[0][0];
-    out[8] = (double)shi[0][0];
-    out[9] = shx[1][0];
-    out[10] = (double)shi[1][0];
-  }
-}
-
-
-// fold part[nparts][11] (threads strided over the parts, then the block tree)
-// into out[11]: summary_final_kernel, and the last workgroup of a fused
-// summary (summary_tail)
-__device__ inline void sum_fold(int nparts, const double* part, double* out) {
-  SumPart p;
-  sum_empty(p);
-  for (int j = threadIdx.x; j < nparts; j += kSumBlock) {
-    const double* q = part + (int64_t)j * kSumParts;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) p.s[k] += q[k];
-    const int64_t ia = (int64_t)q[8], ja = (int64_t)q[10];
-    if (ia >= 0 && (p.imax < 0 || q[7] > p.vmax || (q[7] == p.vmax && ia < p.imax))) p.vmax = q[7], p.imax = ia;
-    if (ja >= 0 && (p.imin < 0 || q[9] < p.vmin || (q[9] == p.vmin && ja < p.imin))) p.vmin = q[9], p.imin = ja;
-  }
-  sum_block_reduce(p, out);
-}
-
 // compute_episode_metrics (utils/metrics.py:264-338) of one episode from its
 // accumulators and env time (the Evaluator's record, eval.py:142-159) into
 // met[QT_MET_ROWS][n] column e: metrics_kernel, and the rollout epilogue of a
@@ -1003,50 +910,16 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   if (FRESH && lc.met) store_metrics(cr, a, t, lc.met, n, ep);  // a fresh pass: the metrics rows (metrics_kernel)
 }
 
-// The fused summary of a fresh pass (LaunchConst::sum_out): workgroup b of
-// the exact pass reduces episodes [b kBlock, (b + 1) kBlock) of the metric
-// rows into sum_work[b][11] (the order of summary_part_kernel with one part
-// per workgroup), and the last workgroup to finish folds all parts into
-// sum_out[11] (summary_final_kernel's order): qt_summary_parts with
-// nparts = the grid bit for bit when kBlock divides n.  Each workgroup's own
-// lanes wrote its episodes' rows (the launch maps slot = episode: no order,
-// no groups, checked on the host) or the fast kernel did, before this launch.
-// Release / acquire at device scope around the per-stream counter make the
-// parts of workgroups on other XCDs visible to the last one; it resets the
-// counter for the next launch on the stream.
-__device__ __forceinline__ void summary_tail(const LaunchConst& lc, int64_t n) {
-  static_assert(kBlock == kSumBlock, "one summary part per rollout workgroup");
-  const int64_t lo = (int64_t)blockIdx.x * kBlock;
-  SumPart p;
-  sum_empty(p);
-  sum_accumulate(p, n, lc.met, 0.0, 0.0, lo, lo + kBlock < n ? lo + kBlock : n);
-  sum_block_reduce(p, lc.sum_work + (int64_t)blockIdx.x * kSumParts);
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    __threadfence();  // this part, before the count
-    const unsigned prev = __hip_atomic_fetch_add(lc.sum_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-    __threadfence();  // the other parts, after the count
-  }
-  __syncthreads();
-  if (!last) return;
-  sum_fold((int)gridDim.x, lc.sum_work, lc.sum_out);
-  if (threadIdx.x == 0) __hip_atomic_store(lc.sum_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
   // the exact pass after a fast flavour that deferred no wave: nothing to do
   // (one uniform load per wave instead of the wave test's ~40 per lane)
-  const bool idle = FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch;
-  const int64_t slot = idle ? -1 : slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
-  if (slot >= 0) rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
-  if (FLAVOR == kExact && lc.sum_out) {  // a fresh pass's fused summary (uniform: a kernel argument)
-    __syncthreads();  // the workgroup's metric rows written
-    summary_tail(lc, b.n);
-  }
+  if (FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch) return;
+  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
+  if (slot < 0) return;
+  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
 }
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type

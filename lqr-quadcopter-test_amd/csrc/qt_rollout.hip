@@ -331,6 +331,81 @@ __global__ __launch_bounds__(kBlock) void metrics_arrays_kernel(qt_criteria cr, 
   for (int i = 0; i < QT_MET_ROWS; ++i) met[i * n + e] = m[i];
 }
 
+// EvaluationSummary partials (utils/metrics.py:341-390): fixed summation
+// order (bitwise reproducible for a given n), first-index argmax/argmin.
+// Partial vector: [7 sums, max, argmax, min, argmin]; an argmax/argmin < 0
+// marks an empty partial.
+constexpr int kSumBlock = 256;
+constexpr int kSumParts = 11;
+
+struct SumPart {
+  double s[7];
+  double vmax, vmin;
+  int64_t imax, imin;
+};
+
+__device__ __forceinline__ void sum_empty(SumPart& p) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) p.s[k] = 0.0;
+  p.vmax = -INFINITY, p.vmin = INFINITY, p.imax = -1, p.imin = -1;
+}
+
+// episodes [lo, hi) of met, strided over the block's threads
+__device__ __forceinline__ void sum_accumulate(SumPart& p, int64_t n, const double* __restrict__ met, double mu_r,
+                                               double mu_e, int64_t lo, int64_t hi) {
+  for (int64_t e = lo + threadIdx.x; e < hi; e += kSumBlock) {
+    const double r = met[QT_MET_ON_TARGET_RATIO * n + e], er = met[QT_MET_MEAN_ERR * n + e];
+    p.s[0] += r;
+    p.s[1] += er;
+    p.s[2] += met[QT_MET_MEAN_EFFORT * n + e];
+    p.s[3] += met[QT_MET_SUCCESS * n + e];
+    p.s[4] += 1.0;
+    p.s[5] += (r - mu_r) * (r - mu_r);
+    p.s[6] += (er - mu_e) * (er - mu_e);
+    if (r > p.vmax || p.imax < 0) p.vmax = r, p.imax = e;
+    if (r < p.vmin || p.imin < 0) p.vmin = r, p.imin = e;
+  }
+}
+
+// tree-combine every thread's partial (fixed pairing); thread 0 writes out[11]
+__device__ void sum_block_reduce(const SumPart& p, double* out) {
+  __shared__ double sh[7][kSumBlock];
+  __shared__ double shx[2][kSumBlock];
+  __shared__ int64_t shi[2][kSumBlock];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] = p.s[k];
+  shx[0][threadIdx.x] = p.vmax;
+  shx[1][threadIdx.x] = p.vmin;
+  shi[0][threadIdx.x] = p.imax;
+  shi[1][threadIdx.x] = p.imin;
+  __syncthreads();
+  for (int w = kSumBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const int o = threadIdx.x + w;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) sh[k][threadIdx.x] += sh[k][o];
+      // keep the lowest index among equal values (np.argmax/argmin first occurrence)
+      const int64_t ia = shi[0][threadIdx.x], ib = shi[0][o];
+      if (ib >= 0 && (ia < 0 || shx[0][o] > shx[0][threadIdx.x] ||
+                      (shx[0][o] == shx[0][threadIdx.x] && ib < ia)))
+        shx[0][threadIdx.x] = shx[0][o], shi[0][threadIdx.x] = ib;
+      const int64_t ja = shi[1][threadIdx.x], jb = shi[1][o];
+      if (jb >= 0 && (ja < 0 || shx[1][o] < shx[1][threadIdx.x] ||
+                      (shx[1][o] == shx[1][threadIdx.x] && jb < ja)))
+        shx[1][threadIdx.x] = shx[1][o], shi[1][threadIdx.x] = jb;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) out[k] = sh[k][0];
+    out[7] = shx[0][0];
+    out[8] = (double)shi[0][0];
+    out[9] = shx[1][0];
+    out[10] = (double)shi[1][0];
+  }
+}
+
 // one workgroup over all episodes
 __global__ __launch_bounds__(kSumBlock) void summary_kernel(int64_t n, const double* __restrict__ met, double mu_r,
                                                             double mu_e, double* out) {
@@ -355,7 +430,17 @@ __global__ __launch_bounds__(kSumBlock) void summary_part_kernel(int64_t n, cons
 // stage 2: one workgroup combines the nparts partials in a fixed order
 __global__ __launch_bounds__(kSumBlock) void summary_final_kernel(int nparts, const double* __restrict__ part,
                                                                   double* out) {
-  sum_fold(nparts, part, out);
+  SumPart p;
+  sum_empty(p);
+  for (int j = threadIdx.x; j < nparts; j += kSumBlock) {
+    const double* q = part + (int64_t)j * kSumParts;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) p.s[k] += q[k];
+    const int64_t ia = (int64_t)q[8], ja = (int64_t)q[10];
+    if (ia >= 0 && (p.imax < 0 || q[7] > p.vmax || (q[7] == p.vmax && ia < p.imax))) p.vmax = q[7], p.imax = ia;
+    if (ja >= 0 && (p.imin < 0 || q[9] < p.vmin || (q[9] == p.vmin && ja < p.imin))) p.vmin = q[9], p.imin = ja;
+  }
+  sum_block_reduce(p, out);
 }
 
 // ------------------------------------------- numpy-order sums (np.add.reduce)
@@ -497,26 +582,6 @@ unsigned long long* defer_flag_for(hipStream_t s) {
   return f;
 }
 
-// Fused-summary workgroup counters, one device word per (device, stream),
-// zeroed on the stream; the last workgroup of each fused summary resets it.
-unsigned* sum_count_for(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> counts;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = counts.find({dev, s});
-  if (it != counts.end()) return it->second;
-  unsigned* f = nullptr;
-  if (hipMalloc(&f, sizeof(*f)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(f, 0, sizeof(*f), s) != hipSuccess) {
-    (void)hipFree(f);
-    return nullptr;
-  }
-  counts[{dev, s}] = f;
-  return f;
-}
-
 // The step flavour a launch can take (launch-level preconditions).
 int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
@@ -532,14 +597,11 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                    double* rec, bool grouped = false, double* reward = nullptr, const double* fresh_off = nullptr,
-                   double* met = nullptr, double* sum_out = nullptr, double* sum_work = nullptr,
-                   unsigned* sum_count = nullptr) {
+                   double* met = nullptr) {
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   lc.hz = make_horizon(e, c, lc.rl);       // the yaw-at-rest loop's safe horizon
   lc.reward = reward;
   lc.fresh_off = fresh_off, lc.met = met;  // qt_rollout_fresh: reset in the prologue, metrics in the epilogue
-  // the fused summary runs in the exact-pass launch only (rollout_kernel's summary_tail)
-  lc.sum_out = sum_out, lc.sum_work = sum_work, lc.sum_count = sum_count;
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
   // rewards are accumulated by the exact step only
@@ -556,50 +618,21 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
   return check_launch();
 }
 
-int rollout_groups(const qt_batch* batch, BatchDev b, bool ff, bool ks, bool no_yaw, const qt_env_params& e,
-                   const qt_ctrl_params& c, const qt_criteria& cr, qt_state st, int nsteps, double* rec, int32_t nseg,
-                   const int32_t* seg_motion, const int64_t* seg_end, hipStream_t s, const double* fresh_off,
-                   double* met);
-
 // qt_rollout / qt_rollout_grouped / qt_rollout_fresh after validation:
 // nseg == 0, one launch set over the batch; else motion groups (wave-aligned
 // segments in one yaw-at-rest launch, or one launch set per group).
 // fresh_off / met: a fresh pass (reset in the prologue, metrics rows in the
-// epilogue); sum_out / sum_work: its summary partials (fused into the exact-
-// pass launch when slot = episode, else summary_part / final launches in the
-// same order).
+// epilogue).
 int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const qt_batch* batch,
                   qt_state st, int nsteps, double* rec, int32_t nseg, const int32_t* seg_motion,
-                  const int64_t* seg_end, hipStream_t s, const double* fresh_off = nullptr, double* met = nullptr,
-                  double* sum_out = nullptr, double* sum_work = nullptr) {
+                  const int64_t* seg_end, hipStream_t s, const double* fresh_off = nullptr, double* met = nullptr) {
   BatchDev b = to_dev(batch);
   const bool ff = c.feedforward_enabled != 0 || batch->ff != nullptr;  // per-episode feed-forward: the FF kernels
   const bool ks = batch->k_structured != 0;
   const bool no_yaw = batch->k_no_yaw != 0;  // yaw-rate gains all zero: yaw stays at rest (dense K too)
-  if (nseg == 0) {
-    // the fused summary needs slot = episode (each workgroup sums the rows its own lanes wrote)
-    unsigned* cnt = (sum_out && !batch->order) ? sum_count_for(s) : nullptr;
-    const int rc = launch_rollout(batch->k_cols, ff, ks, no_yaw, batch->motion ? -1 : e.motion, grid_of(batch->n),
-                                  s, e, c, cr, b, st, nsteps, rec, false, nullptr, fresh_off, met,
-                                  cnt ? sum_out : nullptr, sum_work, cnt);
-    if (rc != QT_OK || !sum_out || cnt) return rc;
-  } else {
-    const int rc = rollout_groups(batch, b, ff, ks, no_yaw, e, c, cr, st, nsteps, rec, nseg, seg_motion, seg_end, s,
-                                  fresh_off, met);
-    if (rc != QT_OK || !sum_out) return rc;
-  }
-  // the summary in its own launches, in the fused order (one part per kBlock episodes)
-  const int parts = grid_of(batch->n);
-  summary_part_kernel<<<parts, kSumBlock, 0, s>>>(batch->n, met, 0.0, 0.0, kBlock, sum_work);
-  summary_final_kernel<<<1, kSumBlock, 0, s>>>(parts, sum_work, sum_out);
-  return check_launch();
-}
-
-// rollout_batch's motion groups
-int rollout_groups(const qt_batch* batch, BatchDev b, bool ff, bool ks, bool no_yaw, const qt_env_params& e,
-                   const qt_ctrl_params& c, const qt_criteria& cr, qt_state st, int nsteps, double* rec, int32_t nseg,
-                   const int32_t* seg_motion, const int64_t* seg_end, hipStream_t s, const double* fresh_off,
-                   double* met) {
+  if (nseg == 0)
+    return launch_rollout(batch->k_cols, ff, ks, no_yaw, batch->motion ? -1 : e.motion, grid_of(batch->n), s, e, c,
+                          cr, b, st, nsteps, rec, false, nullptr, fresh_off, met);
   if (flavor_for(batch->k_cols, ks, no_yaw, e, c, rec) == kYaw0) {
     // every group in one launch, each starting at a wavefront boundary (BatchDev's
     // wave-aligned segments; both the fast kernel and its exact pass map slots so)
@@ -720,13 +753,12 @@ int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, con
 }
 
 int qt_rollout_fresh(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
-                     const qt_batch* batch, const double* offset, qt_state st, int32_t nsteps, double* met,
-                     double* summary, double* summary_work, int32_t nseg, const int32_t* seg_motion,
-                     const int64_t* seg_end, void* stream) {
+                     const qt_batch* batch, const double* offset, qt_state st, int32_t nsteps, double* met, int32_t nseg,
+                     const int32_t* seg_motion, const int64_t* seg_end, void* stream) {
   if (!env || !ctrl || !crit || !batch || batch->n < 0 || nsteps < 0 || !batch->K) return QT_EINVAL;
   if (batch->k_cols != 3 && batch->k_cols != 6 && batch->k_cols != 9) return QT_EINVAL;
   if (batch->n == 0) return QT_OK;  // empty: no per-episode pointer is read
-  if (!offset || !met || !valid_state(st, batch->k_cols != 6) || (summary && !summary_work)) return QT_EINVAL;
+  if (!offset || !met || !valid_state(st, batch->k_cols != 6)) return QT_EINVAL;
   if (nseg < 0 || (nseg > 0 && (!seg_motion || !seg_end))) return QT_EINVAL;
   int64_t prev = 0;
   for (int32_t i = 0; i < nseg; ++i) {
@@ -738,15 +770,9 @@ int qt_rollout_fresh(const qt_env_params* env, const qt_ctrl_params* ctrl, const
   if (nsteps == 0) {  // nothing to run: the reset and the metrics of the reset state
     reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(*env, to_dev(batch), offset, st);
     metrics_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(*crit, batch->n, st.acc, st.t, met);
-    if (summary) {
-      const int parts = grid_of(batch->n);
-      summary_part_kernel<<<parts, kSumBlock, 0, s>>>(batch->n, met, 0.0, 0.0, kBlock, summary_work);
-      summary_final_kernel<<<1, kSumBlock, 0, s>>>(parts, summary_work, summary);
-    }
     return check_launch();
   }
-  return rollout_batch(*env, *ctrl, *crit, batch, st, nsteps, nullptr, nseg, seg_motion, seg_end, s, offset, met,
-                       summary, summary_work);
+  return rollout_batch(*env, *ctrl, *crit, batch, st, nsteps, nullptr, nseg, seg_motion, seg_end, s, offset, met);
 }
 
 int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* action, qt_state st, double* err,

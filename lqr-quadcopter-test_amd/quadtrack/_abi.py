@@ -111,8 +111,8 @@ def load():
     L.qt_rollout_rewards.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, vp]
     L.qt_rollout_grouped.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), State, i32, vp, i32,
                                      P(C.c_int32), P(C.c_int64), vp]
-    L.qt_rollout_fresh.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), vp, State, i32, vp, vp, vp,
-                                   i32, P(C.c_int32), P(C.c_int64), vp]
+    L.qt_rollout_fresh.argtypes = [P(EnvParams), P(CtrlParams), P(Criteria), P(Batch), vp, State, i32, vp, i32,
+                                   P(C.c_int32), P(C.c_int64), vp]
     L.qt_seed_uniform.argtypes = [i64, vp, i32, vp, vp, vp, vp]
     L.qt_env_step.argtypes = [P(EnvParams), P(Batch), vp, State, vp, vp, vp, vp, vp, vp]
     L.qt_compute_action.argtypes = [P(CtrlParams), P(Batch), vp, vp, vp, vp, vp, vp]

@@ -312,15 +312,11 @@ def rollout(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatc
 
 
 def rollout_fresh(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState,
-                  nsteps: int, met: torch.Tensor | None = None, summary: bool = False):
+                  nsteps: int, met: torch.Tensor | None = None) -> torch.Tensor:
     """reset -> rollout(nsteps) -> episode_metrics as one launch set
     (qt_rollout_fresh, ABI 8): the rollout kernel forms the reset state from
     batch.offset in its prologue and writes the metrics rows in its epilogue.
-    Same results as the three calls, bit for bit.  Returns met [MET_ROWS, n];
-    with summary=True (met, partials[11]): summary_partials' values summed one
-    part per 256 episodes (bitwise summary_partials(met, nparts=n // 256) when
-    256 divides n), reduced inside the exact-pass launch when the batch has no
-    order / groups."""
+    Same results as the three calls, bit for bit.  Returns met [MET_ROWS, n]."""
     lib = _abi.load()
     n = batch.n
     if met is None:
@@ -333,17 +329,11 @@ def rollout_fresh(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: Episo
         nseg = len(seg_motion)
         sm = (C.c_int32 * nseg)(*[int(v) for v in seg_motion])
         se = (C.c_int64 * nseg)(*[int(v) for v in seg_end])
-    out = work = None
-    if summary and n == 0:
-        return met, summary_partials(met)  # the empty partial
-    if summary:
-        out = torch.empty(11, dtype=F64, device=batch.device)
-        work = torch.empty(max(1, -(-n // 256)) * 11, dtype=F64, device=batch.device)
     with torch.cuda.device(batch.device):
         check(lib.qt_rollout_fresh(C.byref(env), C.byref(ctrl), C.byref(crit), C.byref(batch.c_batch()),
-                                   ptr(batch.offset), st.c_state(), int(nsteps), ptr(met), ptr(out), ptr(work), nseg,
-                                   sm, se, stream_of(batch.device)), "qt_rollout_fresh")
-    return (met, out) if summary else met
+                                   ptr(batch.offset), st.c_state(), int(nsteps), ptr(met), nseg, sm, se,
+                                   stream_of(batch.device)), "qt_rollout_fresh")
+    return met
 
 
 def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: EpisodeBatch, st: RolloutState,

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Same-box A/B of the bench pass forms (config 2, 65,536 episodes): the
+fresh launch with the summary fused into the exact-pass launch, against the
+fresh launch followed by qt_summary_parts' two launches (same partition) and
+against the unfused reset / rollout / metrics / summary sequence.  Prints one
+JSON line per form: ms per pass over --passes back-to-back passes after a
+1 s warm-up, best of --repeat."""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "lqr-quadcopter-test_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--passes", type=int, default=100)
+    ap.add_argument("--repeat", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.env.config import EnvConfig
+    from quadtrack.rollout import build_batch, max_steps_for
+
+    dev = torch.device("cuda", 0)
+    n = 65536
+    cfg = EnvConfig.from_dict({"target": {"motion_type": "linear"}})
+    env, crit = cfg.to_params(), core.criteria()
+    ctl = BatchedRiccatiLQR({"dt": 0.01}, device=dev)
+    batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+    st = core.RolloutState.empty(n, dev)
+    nsteps = max_steps_for(env)
+    nparts = n // 256
+
+    forms = {
+        "fused_summary": lambda: core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps, summary=True),
+        "fresh_then_summary_parts": lambda: core.summary_partials(
+            core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps), nparts=nparts),
+        "unfused": lambda: (core.reset(env, batch, st), core.rollout(env, ctl.ctrl, crit, batch, st, nsteps),
+                            core.summary_partials(core.episode_metrics(crit, st), nparts=nparts)),
+    }
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:
+        for f in forms.values():
+            f()
+        torch.cuda.synchronize()
+    for name, f in forms.items():
+        best = None
+        for _ in range(args.repeat):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(args.passes):
+                f()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t) / args.passes * 1e3
+            best = ms if best is None else min(best, ms)
+        print(json.dumps({"form": name, "ms_per_pass": round(best, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -39,22 +39,15 @@ def _both(ctl, env_cfg, n, nsteps, motion=None, plant_mass=None, poison=None):
     for fresh in (True, False):
         st = core.RolloutState.empty(n, batch.device)
         if fresh:
-            met, part = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps, summary=True)
+            met = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps)
         else:
             core.reset(env, batch, st)
             core.rollout(env, ctl.ctrl, crit, batch, st, nsteps)
             met = core.episode_metrics(crit, st)
-            part = core.summary_partials(met, nparts=max(1, -(-n // 256)))
         torch.cuda.synchronize()
-        out.append([t.cpu().numpy() for t in (met, st.x, st.target, st.t, st.acc, st.integ, part)])
-    for a, b in zip(out[0][:-1], out[1][:-1]):
+        out.append([t.cpu().numpy() for t in (met, st.x, st.target, st.t, st.acc, st.integ)])
+    for a, b in zip(*out):
         np.testing.assert_array_equal(a, b)
-    # the fused summary sums 256 episodes per part; qt_summary_parts splits n
-    # evenly over its parts, the same split when 256 divides n
-    if n % 256 == 0:
-        np.testing.assert_array_equal(out[0][-1], out[1][-1])
-    else:
-        np.testing.assert_allclose(out[0][-1], out[1][-1], rtol=1e-13, atol=0)
     return out[0][0]
 
 
@@ -126,33 +119,3 @@ def test_fresh_pass_edges(qt, n, nsteps):
         return
     met = _both(BatchedRiccatiLQR({"dt": 0.01}), {"target": {"motion_type": "linear"}}, n, nsteps)
     assert np.all(met == 0.0)
-
-
-def test_fresh_summary_repeated_and_ordered(qt):
-    """The fused summary's per-stream workgroup counter resets itself: ten
-    passes in a row on one stream give the same partials; a batch with a
-    permuting `order` takes the separate summary launches, same values."""
-    from quadtrack import core
-    from quadtrack.controllers import BatchedRiccatiLQR
-    from quadtrack.env.config import EnvConfig
-    from quadtrack.rollout import build_batch
-
-    n = 1000
-    cfg = EnvConfig.from_dict({"target": {"motion_type": "circular"}})
-    env, crit = cfg.to_params(), core.criteria()
-    ctl = BatchedRiccatiLQR({"dt": 0.01})
-    batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
-    st = core.RolloutState.empty(n, batch.device)
-    parts = [core.rollout_fresh(env, ctl.ctrl, crit, batch, st, 600, summary=True)[1].cpu().numpy() for _ in range(10)]
-    for p in parts[1:]:
-        np.testing.assert_array_equal(p, parts[0])
-    # a permuting `order`: the summary in its own launches, in the fused order
-    # (the same rows: episode e's metrics do not depend on its slot)
-    perm = np.random.default_rng(0).permutation(n).astype(np.int32)
-    ob = build_batch(ctl, cfg, n, seeds=np.arange(n), order=perm)
-    met, part = core.rollout_fresh(env, ctl.ctrl, crit, ob, core.RolloutState.empty(n, ob.device), 600, summary=True)
-    ref_met, ref_part = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, 600, summary=True)
-    np.testing.assert_array_equal(met.cpu().numpy(), ref_met.cpu().numpy())
-    np.testing.assert_array_equal(part.cpu().numpy(), ref_part.cpu().numpy())
-    met0, part0 = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, 0, summary=True)
-    assert float(part0[4]) == n and float(part0[0]) == 0.0
