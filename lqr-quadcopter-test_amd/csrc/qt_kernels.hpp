@@ -725,8 +725,8 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
                fmax(t - e.max_episode_time, -(double)rem));
       return __builtin_amdgcn_ballot_w64(stop_m >= 0.0) != 0;
     };
-    // The safe horizon's steps without the vote (in pairs: one back edge per
-    // two steps), then one voted step.
+    // The safe horizon's steps without the vote (four per back edge; two
+    // with the folded rotor), then one voted step.
     do {
       const int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
       if constexpr (kFold) {
