@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Same-box A/B of the bench pass forms (config 2, 65,536 episodes): the
-fresh launch with the summary fused into the exact-pass launch, against the
-fresh launch followed by qt_summary_parts' two launches (same partition) and
-against the unfused reset / rollout / metrics / summary sequence.  Prints one
+fresh launch with the summary fused into the exact-pass launch (where the
+library has it), the fresh launch followed by qt_summary_parts' two launches,
+the same with the summary on a side stream behind each pass (two buffers,
+bench.py's form), and the unfused reset / rollout / metrics / summary
+sequence.  Prints one
 JSON line per form: ms per pass over --passes back-to-back passes after a
 1 s warm-up, best of --repeat."""
 
@@ -41,12 +43,35 @@ def main():
     nparts = n // 256
 
     forms = {
-        "fused_summary": lambda: core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps, summary=True),
         "fresh_then_summary_parts": lambda: core.summary_partials(
             core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps), nparts=nparts),
         "unfused": lambda: (core.reset(env, batch, st), core.rollout(env, ctl.ctrl, crit, batch, st, nsteps),
                             core.summary_partials(core.episode_metrics(crit, st), nparts=nparts)),
     }
+    # the bench's form: two buffers, the summary on a side stream behind each
+    # pass, overlapping the next pass's rollout
+    st2 = [st, core.RolloutState.empty(n, dev)]
+    mets = [torch.empty(core.MET_ROWS, n, dtype=torch.float64, device=dev) for _ in range(2)]
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    free = [None, None]
+    k = [0]
+
+    def pipelined():
+        b = k[0] % 2
+        k[0] += 1
+        if free[b] is not None:
+            main.wait_event(free[b])
+        met = core.rollout_fresh(env, ctl.ctrl, crit, batch, st2[b], nsteps, met=mets[b])
+        done = torch.cuda.Event()
+        done.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(done)
+            core.summary_partials(met, nparts=nparts)
+            free[b] = torch.cuda.Event()
+            free[b].record(side)
+
+    forms["fresh_pipelined_summary"] = pipelined
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 1.0:
         for f in forms.values():
