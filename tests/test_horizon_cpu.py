@@ -113,3 +113,46 @@ def test_horizon_step_bounds_hold(case):
     # not vacuous: the saturating cases reach a good part of each bound
     if name in ("lqr_far", "no_drag_fast"):
         assert worst[0] > 0.3 and worst[2] > 0.3, worst
+
+
+def tie_binade(dt):
+    """make_horizon's tie binade (qt_device.hpp): dt = m 2^q with m odd; the
+    exponent E of the t binade [2^E, 2^(E+1)) whose ulp is 2^(q+1)."""
+    m, q = np.frexp(dt)
+    m, q = int(m * 2.0**53), int(q) - 53
+    while m % 2 == 0:
+        m //= 2
+        q += 1
+    return q + 53
+
+
+@pytest.mark.parametrize("dt", [0.01, 0.005, 0.02, 1.0 / 64, 0.1, 0.001])
+def test_time_step_constant_per_binade(dt):
+    """The folded target rotor (qt_kernels.hpp rotor_fold) rests on this: in
+    every binade of t but the tie binade, fl(t + dt) - t is one value (t is a
+    multiple of the binade's ulp), and the horizon never crosses a binade
+    edge.  Checked over the steps of episodes started at an even and at an
+    odd multiple of each binade's ulp; in the tie binade round-half-even
+    gives two values, by the parity of t's last bit."""
+    e_tie = tie_binade(dt)
+    seen_tie = False
+    for e in range(-8, 8):
+        lo, hi = 2.0**e, 2.0**(e + 1)
+        if hi <= dt:
+            continue
+        steps = set()
+        for t in (lo, np.nextafter(lo, hi)):
+            k = 0
+            while t + dt < hi and k < 4000:
+                t1 = t + dt
+                steps.add(t1 - t)
+                t = t1
+                k += 1
+        if not steps:
+            continue
+        if e == e_tie:
+            assert len(steps) == 2, (dt, e)
+            seen_tie = True
+        else:
+            assert len(steps) == 1, (dt, e, sorted(steps)[:3])
+    assert seen_tie or not (-8 <= e_tie < 8)
