@@ -725,14 +725,20 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
                fmax(t - e.max_episode_time, -(double)rem));
       return __builtin_amdgcn_ballot_w64(stop_m >= 0.0) != 0;
     };
-    // The safe horizon's steps without the vote (four per back edge; two
-    // with the folded rotor), then one voted step.
+    // The safe horizon's steps without the vote (four per back edge, then
+    // the horizon's last two), then one voted step.
     do {
       const int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
       if constexpr (kFold) {
         double fc[3], fs[3];  // the horizon's folded target rotor
         rotor_fold<MOTION>(k, ((t + e.dt) - t) - e.dt, fc, fs);
-        for (int j = 0; j < H; j += 2) {
+        for (int j = 4; j <= H; j += 4) {
+          step(std::false_type{}, fc, fs);
+          step(std::false_type{}, fc, fs);
+          step(std::false_type{}, fc, fs);
+          step(std::false_type{}, fc, fs);
+        }
+        if (H & 2) {
           step(std::false_type{}, fc, fs);
           step(std::false_type{}, fc, fs);
         }

@@ -54,9 +54,8 @@ def step_loops(blocks):
 
 
 def row(tag, motion, pair, voted):
-    """The no-vote loop runs four steps per back edge (two in the LQI loops
-    with the folded target rotor): told apart by its size against the voted
-    step's."""
+    """The no-vote loop runs four steps per back edge (two in older builds):
+    told apart by its size against the voted step's."""
     v = f"{voted['n']:5d} {voted['valu']:5d} {voted['salu']:5d}" if voted else "    -     -     -"
     k = 4 if voted and pair["n"] > 2.5 * voted["n"] else 2
     print(f"{tag:46s} {motion:11s} {pair['n'] / k:6.1f} {pair['valu'] / k:6.1f} {pair['salu'] / k:5.1f}   {v}")
