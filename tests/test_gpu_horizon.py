@@ -1,0 +1,59 @@
+"""The yaw-at-rest loop's safe horizon under randomised limits: fast flavour
+(horizon, no per-step vote) against the exact step (recording forces it) on
+the same episodes, for 12 seeded configurations that push each stop
+condition into the horizons — low speed clamps, close position bounds, odd
+episode lengths, other time steps and rate limits, light and heavy plants,
+LQR / LQI / PID.  Decisions (steps, termination codes, counts) must be
+identical, values within 1e-9 (the two paths contract FMAs differently).
+GPU only."""
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import FIELDS
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def qt():
+    import quadtrack
+
+    quadtrack._abi.require_gpu()
+    return quadtrack
+
+
+def _config(i):
+    r = np.random.default_rng(1000 + i)
+    motion = ["stationary", "linear", "circular", "sinusoidal", "figure8"][i % 5]
+    dt = float(r.choice([0.005, 0.01, 0.02]))
+    env = {"target": {"motion_type": motion, "speed": float(r.uniform(0.5, 4.0))},
+           "simulation": {"dt": dt, "max_velocity": float(r.uniform(2.0, 8.0)),
+                          "max_position": float(r.uniform(3.0, 30.0)),
+                          "max_episode_time": float(np.round(r.uniform(4.0, 12.0), 3))},
+           "quadcopter": {"max_angular_rate": 3.0}}
+    kind = ["riccati_lqr", "lqi", "pid"][i % 3]
+    ctl = {"dt": dt, "max_rate": float(r.uniform(1.0, 3.0))}
+    if kind == "riccati_lqr":
+        ctl.update(q_pos=[float(r.uniform(1e-4, 5.0))] * 2 + [16.0])
+    mass = r.uniform(0.4, 2.0, 256)
+    return env, kind, ctl, mass
+
+
+@pytest.mark.parametrize("i", range(12))
+def test_horizon_randomised_limits(qt, i):
+    from quadtrack.controllers import batched_controller
+    from quadtrack.rollout import run_closed_loop
+
+    env, kind, ctl_cfg, mass = _config(i)
+    ctl = batched_controller(kind, ctl_cfg)
+    n = 256
+    fast = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), plant_mass=mass)
+    exact = run_closed_loop(ctl, env, n=n, seeds=np.arange(n), plant_mass=mass, record=True)
+    mf, me = fast.metrics.cpu().numpy(), exact.metrics.cpu().numpy()
+    for k, f in enumerate(FIELDS):
+        if f in ("overshoot_count", "success", "termination_code", "action_violations", "steps"):
+            np.testing.assert_array_equal(mf[k], me[k], err_msg=f)
+        else:
+            np.testing.assert_allclose(mf[k], me[k], rtol=1e-9, atol=1e-9, err_msg=f)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy(), exact.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
