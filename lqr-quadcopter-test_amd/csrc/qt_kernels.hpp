@@ -726,7 +726,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       return __builtin_amdgcn_ballot_w64(stop_m >= 0.0) != 0;
     };
     // The safe horizon's steps without the vote (four per back edge, then
-    // the horizon's last two), then one voted step.
+    // the horizon's last two); voted steps only where no horizon is left.
     do {
       const int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
       if constexpr (kFold) {
@@ -756,10 +756,12 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
         }
       }
       rem -= H;
-      // a wave with a lane near a stop (H = 0) takes a few voted steps before
-      // it bounds the horizon again; without a horizon (hz.on == 0: a
-      // non-finite limit) every step is voted
-      const int nv = H > 0 ? 1 : (k.hz.on ? kVotedBurst : (1 << 30));
+      // Horizons chain: the state after a horizon's steps is one no lane
+      // stopped at, so the next horizon is bounded from it directly.  Only a
+      // wave with a lane near a stop (H = 0) takes voted steps, a few before
+      // it bounds again; without a horizon (hz.on == 0: a non-finite limit)
+      // every step is voted.
+      const int nv = H > 0 ? 0 : (k.hz.on ? kVotedBurst : (1 << 30));
       bool stop = false;
       for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{}, nullptr, nullptr);
       if (stop) break;
