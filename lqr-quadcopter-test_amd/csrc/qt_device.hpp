@@ -522,8 +522,10 @@ struct Horizon {
 QT_HD Horizon make_horizon(const qt_env_params& e, const qt_ctrl_params& c, const RateLin& rl) {
   Horizon h{};
   const double tm = fmax(fabs(c.min_thrust), fabs(c.max_thrust));
-  const bool ok = e.max_velocity > 0.0 && e.max_velocity < 1e150 && e.max_position > 0.0 &&
-                  e.max_position < 1e150 && e.dt > 0.0 && e.dt < 1e3 && fabs(e.max_episode_time) < 1e150 &&
+  // (limits bounded away from 0 and infinity, so every per-step bound and its
+  // reciprocal in yaw0_horizon is a finite positive number)
+  const bool ok = e.max_velocity > 1e-100 && e.max_velocity < 1e150 && e.max_position > 1e-100 &&
+                  e.max_position < 1e150 && e.dt > 1e-100 && e.dt < 1e3 && fabs(e.max_episode_time) < 1e150 &&
                   tm < 1e150 && c.max_rate >= 0.0 && c.max_rate < 1e150;
   if (!ok) return h;
   h.on = 1;
