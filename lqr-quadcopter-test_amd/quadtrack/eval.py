@@ -275,53 +275,57 @@ def run_hyperparameter_sweep(sweep_config_path: str | Path, output_dir: str | Pa
     import yaml
 
     with open(sweep_config_path) as f:
-        sweep_config = yaml.safe_load(f)
-    output_dir = Path(output_dir)
-    output_dir.mkdir(parents=True, exist_ok=True)
-    results = []
-    configs = sweep_config.get("configurations", [])
-    logger.info("Running sweep with %d configurations", len(configs))
-    for i, config in enumerate(configs):
-        name = config.get("name", f"config_{i}")
-        logger.info("Configuration %d/%d: %s", i + 1, len(configs), config.get("name"))
-        try:
-            controller = load_controller(controller_type=config.get("controller_type", "deep"),
-                                         checkpoint_path=config.get("checkpoint_path"),
-                                         config=config.get("controller_config"))
-            env_config = EnvConfig.from_dict(config["env_config"]) if "env_config" in config else EnvConfig()
-            criteria = SuccessCriteria()
-            if "criteria" in config:
-                crit = config["criteria"]
-                criteria = SuccessCriteria(min_on_target_ratio=crit.get("min_on_target_ratio", 0.8),
-                                           min_episode_duration=crit.get("min_episode_duration", 30.0),
-                                           target_radius=crit.get("target_radius", 0.5))
-            num_episodes, seed = config.get("num_episodes", 5), config.get("seed", 42)
-            if batched is True or (batched == "auto" and _stateless(controller)):
-                (output_dir / name / "plots").mkdir(parents=True, exist_ok=True)  # as Evaluator() makes them
-                summary = evaluate_batched(controller, env_config, num_episodes=num_episodes, base_seed=seed,
-                                           criteria=criteria, with_episode_metrics=False)
-            else:
-                evaluator = Evaluator(controller=controller, env_config=env_config, criteria=criteria,
-                                      output_dir=output_dir / name)
-                summary = evaluator.evaluate(num_episodes=num_episodes, base_seed=seed, verbose=False)
-            results.append({"name": name, "config": config, "mean_on_target_ratio": summary.mean_on_target_ratio,
-                            "success_rate": summary.success_rate, "mean_tracking_error": summary.mean_tracking_error,
-                            "meets_criteria": summary.meets_criteria})
-            logger.info("  Result: on-target=%.1f%%, success=%.1f%%", summary.mean_on_target_ratio * 100,
-                        summary.success_rate * 100)
-        except Exception as e:  # eval.py:592-601
-            logger.error("Configuration %s failed: %s", config.get("name"), e)
-            results.append({"name": name, "config": config, "error": str(e)})
-    valid_results = [r for r in results if "error" not in r]
-    valid_results.sort(key=lambda x: x["mean_on_target_ratio"], reverse=True)
-    sweep_results_path = output_dir / "sweep_results.json"
-    with open(sweep_results_path, "w") as f:
-        json.dump(valid_results, f, indent=2)
-    logger.info("Saved sweep results: %s", sweep_results_path)
-    print("\n" + "=" * 60)
-    print("HYPERPARAMETER SWEEP RESULTS (Ranked)")
-    print("=" * 60)
-    for k, r in enumerate(valid_results):
-        print(f"{k + 1}. {r['name']}: on-target={r['mean_on_target_ratio']:.1%}, success={r['success_rate']:.1%}")
-    print("=" * 60)
-    return valid_results
+        entries = (yaml.safe_load(f) or {}).get("configurations", [])
+    out = Path(output_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    logger.info("Running sweep with %d configurations", len(entries))
+    outcomes = []
+    for i, entry in enumerate(entries):
+        logger.info("Configuration %d/%d: %s", i + 1, len(entries), entry.get("name"))
+        outcomes.append(_sweep_entry(entry, entry.get("name", f"config_{i}"), out, batched))
+    ranked = sorted((r for r in outcomes if "error" not in r), key=lambda r: r["mean_on_target_ratio"], reverse=True)
+    path = out / "sweep_results.json"
+    path.write_text(json.dumps(ranked, indent=2))
+    logger.info("Saved sweep results: %s", path)
+    bar = "=" * 60
+    lines = [f"{k}. {r['name']}: on-target={r['mean_on_target_ratio']:.1%}, success={r['success_rate']:.1%}"
+             for k, r in enumerate(ranked, 1)]
+    print("\n".join(["", bar, "HYPERPARAMETER SWEEP RESULTS (Ranked)", bar, *lines, bar]))
+    return ranked
+
+
+def _sweep_criteria(entry: dict) -> SuccessCriteria:
+    """A sweep entry's `criteria` block over the SuccessCriteria defaults."""
+    crit = entry.get("criteria")
+    if crit is None:
+        return SuccessCriteria()
+    return SuccessCriteria(min_on_target_ratio=crit.get("min_on_target_ratio", 0.8),
+                           min_episode_duration=crit.get("min_episode_duration", 30.0),
+                           target_radius=crit.get("target_radius", 0.5))
+
+
+def _sweep_entry(entry: dict, name: str, out: Path, batched) -> dict:
+    """One sweep configuration: its result row, or an `error` row when building
+    or evaluating it raises (eval.py:592-601 logs and keeps going)."""
+    try:
+        controller = load_controller(controller_type=entry.get("controller_type", "deep"),
+                                     checkpoint_path=entry.get("checkpoint_path"),
+                                     config=entry.get("controller_config"))
+        env_config = EnvConfig.from_dict(entry["env_config"]) if "env_config" in entry else EnvConfig()
+        criteria = _sweep_criteria(entry)
+        episodes, seed = entry.get("num_episodes", 5), entry.get("seed", 42)
+        if batched is True or (batched == "auto" and _stateless(controller)):
+            (out / name / "plots").mkdir(parents=True, exist_ok=True)  # the directories Evaluator() makes
+            summary = evaluate_batched(controller, env_config, num_episodes=episodes, base_seed=seed,
+                                       criteria=criteria, with_episode_metrics=False)
+        else:
+            summary = Evaluator(controller=controller, env_config=env_config, criteria=criteria,
+                                output_dir=out / name).evaluate(num_episodes=episodes, base_seed=seed, verbose=False)
+    except Exception as e:
+        logger.error("Configuration %s failed: %s", entry.get("name"), e)
+        return {"name": name, "config": entry, "error": str(e)}
+    logger.info("  Result: on-target=%.1f%%, success=%.1f%%", summary.mean_on_target_ratio * 100,
+                summary.success_rate * 100)
+    return {"name": name, "config": entry, "mean_on_target_ratio": summary.mean_on_target_ratio,
+            "success_rate": summary.success_rate, "mean_tracking_error": summary.mean_tracking_error,
+            "meets_criteria": summary.meets_criteria}

@@ -53,24 +53,35 @@ from .utils.metrics import SuccessCriteria
 logger = logging.getLogger(__name__)
 
 
+# substrings a result / resume path may not contain, with the reference's
+# messages (tuning.py:64-106)
+_PATH_REFUSED = (
+    ("..", "Path contains path traversal sequence '..': {p}. "
+           "Use absolute paths or paths without parent directory references."),
+    ("\x00", "Path contains null byte: {p}"),
+)
+
+
 def _validate_path(path: Path) -> None:
-    """Path checks of tuning.py:64-106: no '..' or NUL, resolvable."""
-    path_str = str(path)
-    if ".." in path_str:
-        raise ValueError(f"Path contains path traversal sequence '..': {path}. "
-                         "Use absolute paths or paths without parent directory references.")
-    if "\x00" in path_str:
-        raise ValueError(f"Path contains null byte: {path}")
+    """Path checks of tuning.py:64-106: no '..' or NUL; resolvable; a relative
+    path may leave the working directory only to somewhere below the root."""
+    for token, message in _PATH_REFUSED:
+        if token in str(path):
+            raise ValueError(message.format(p=path))
     try:
         resolved = path.resolve()
-        if not path.is_absolute():
-            try:
-                resolved.relative_to(Path.cwd().resolve())
-            except ValueError:
-                if len(resolved.parts) < 2:
-                    raise ValueError(f"Relative path resolves outside working directory: {path}")
+        if path.is_absolute() or len(resolved.parts) >= 2:
+            return
+        inside = True
+        try:
+            resolved.relative_to(Path.cwd().resolve())
+        except ValueError:
+            inside = False
     except (OSError, RuntimeError) as e:
         raise ValueError(f"Cannot resolve path {path}: {e}")
+    if not inside:
+        raise ValueError(f"Relative path resolves outside working directory: {path}")
+
 
 # parameter name -> (range attribute, components); the order of
 # _generate_random_config (tuning.py:689-733)
