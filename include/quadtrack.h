@@ -258,7 +258,9 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    at a 64-lane wave boundary, so every wave takes the loop specialised for its
    motion (<= 8 non-empty groups; more fall back to one launch per group);
    other flavours launch once per group.  Results are identical to
-   qt_rollout's. */
+   qt_rollout's.  seg_motion must agree with batch->motion (when given) for
+   every slot; a wave holding a slot whose batch->motion differs is run by the
+   exact pass, which takes each episode's motion from batch->motion. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);

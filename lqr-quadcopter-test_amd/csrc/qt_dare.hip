@@ -834,10 +834,361 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVE
   }
 }
 
-// Launch the group kernel sized for (n, p): 6 / 4, 9 / 4, else 16 / 8.
+// ------------------------------------------------------- row kernel
+//
+// The same dense SDA with its products in registers.  One problem per DPP
+// row (16 lanes, 4 problems per wavefront), lane r holding row r of H, A and
+// G for the whole solve.  A product X Y (row r: sum_l X[r][l] Y[l][:]) reads
+// Y's row l from lane l of the row by DPP row_newbcast — the one DPP control
+// gfx950 applies to 64-bit operands — so the doubling's eight products are
+// register-to-register (no LDS traffic, no LDS latency); X Y' (row r, entry j:
+// sum_l X[r][l] Y[j][l]) broadcasts lane j instead.  LDS is left with what
+// moves data between lanes by a data-dependent or transposed pattern: the
+// inversion's pivot rows (the pivot lane is chosen at run time), the
+// inverse's row / column permutation, and three transposes per doubling
+// (A' for A' H Y1, and the two symmetrisations).  Validation, G = B R^-1 B'
+// and the final gain are the group kernel's code (once per problem).
+
+// v_fmac_f64 with its first source broadcast from lane l of each DPP row
+// (row_newbcast: the DPP control gfx950 applies to 64-bit operands), N per
+// block.  Written as inline asm because the compiler does not fold a 64-bit
+// DPP move into the FMA (it would issue a v_mov_b64_dpp per product term).
+// Each block opens with s_nop 4: a DPP source VGPR written by the VALU needs
+// 2 wait states and an EXEC write 5, and the compiler's hazard recognizer
+// does not look inside inline asm.
+#define QT_FR(i) "v_fmac_f64_dpp %[a" #i "], %[y" #i "], %[x] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+#define QT_FC(i) "v_fmac_f64_dpp %[a" #i "], %[y], %[x] row_newbcast:" #i " row_mask:0xf bank_mask:0xf\n\t"
+#define QT_A(i) [a##i] "+v"(a[i])
+#define QT_Y(i) [y##i] "v"(y[i])
+#define QT_FR6 QT_FR(0) QT_FR(1) QT_FR(2) QT_FR(3) QT_FR(4) QT_FR(5)
+#define QT_FC6 QT_FC(0) QT_FC(1) QT_FC(2) QT_FC(3) QT_FC(4) QT_FC(5)
+#define QT_A6 QT_A(0), QT_A(1), QT_A(2), QT_A(3), QT_A(4), QT_A(5)
+#define QT_Y6 QT_Y(0), QT_Y(1), QT_Y(2), QT_Y(3), QT_Y(4), QT_Y(5)
+#define QT_FR9 QT_FR6 QT_FR(6) QT_FR(7) QT_FR(8)
+#define QT_FC9 QT_FC6 QT_FC(6) QT_FC(7) QT_FC(8)
+#define QT_A9 QT_A6, QT_A(6), QT_A(7), QT_A(8)
+#define QT_Y9 QT_Y6, QT_Y(6), QT_Y(7), QT_Y(8)
+#define QT_FR16 QT_FR9 QT_FR(9) QT_FR(10) QT_FR(11) QT_FR(12) QT_FR(13) QT_FR(14) QT_FR(15)
+#define QT_FC16 QT_FC9 QT_FC(9) QT_FC(10) QT_FC(11) QT_FC(12) QT_FC(13) QT_FC(14) QT_FC(15)
+#define QT_A16 QT_A9, QT_A(9), QT_A(10), QT_A(11), QT_A(12), QT_A(13), QT_A(14), QT_A(15)
+#define QT_Y16 QT_Y9, QT_Y(9), QT_Y(10), QT_Y(11), QT_Y(12), QT_Y(13), QT_Y(14), QT_Y(15)
+
+// a[j] += Y[L][j] x for j < N, row L of Y in lane L's y
+template <int N, int L>
+__device__ __forceinline__ void fmac_row(double* a, const double* y, double x) {
+  static_assert(N == 6 || N == 9 || N == 16, "row block sizes");
+  if constexpr (N == 6)
+    asm("s_nop 4\n\t" QT_FR6 : QT_A6 : QT_Y6, [x] "v"(x), [l] "n"(L));
+  else if constexpr (N == 9)
+    asm("s_nop 4\n\t" QT_FR9 : QT_A9 : QT_Y9, [x] "v"(x), [l] "n"(L));
+  else
+    asm("s_nop 4\n\t" QT_FR16 : QT_A16 : QT_Y16, [x] "v"(x), [l] "n"(L));
+}
+
+// a[l] += Y[l][j] x for l < N, entry j of row l of Y in lane l's yj
+template <int N>
+__device__ __forceinline__ void fmac_col(double* a, double yj, double x) {
+  static_assert(N == 6 || N == 9 || N == 16, "column block sizes");
+  if constexpr (N == 6)
+    asm("s_nop 4\n\t" QT_FC6 : QT_A6 : [y] "v"(yj), [x] "v"(x));
+  else if constexpr (N == 9)
+    asm("s_nop 4\n\t" QT_FC9 : QT_A9 : [y] "v"(yj), [x] "v"(x));
+  else
+    asm("s_nop 4\n\t" QT_FC16 : QT_A16 : [y] "v"(yj), [x] "v"(x));
+}
+
+// acc[j] += sum_l x[l] Y[l][j] (l, j < N), row l of Y in lane l's y
+template <int N, int L = 0>
+__device__ __forceinline__ void bmul_acc(const double* x, const double* y, double* acc) {
+  if constexpr (L < N) {
+    fmac_row<N, L>(acc, y, x[L]);
+    bmul_acc<N, L + 1>(x, y, acc);
+  }
+}
+
+// out = x Y (row r of the product)
+template <int N>
+__device__ __forceinline__ void bmul(const double* x, const double* y, double* out) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = 0.0;
+  bmul_acc<N>(x, y, out);
+}
+
+// out = x Y' (out[l] = sum_j x[j] Y[l][j]), row l of Y in lane l's y
+template <int N>
+__device__ __forceinline__ void bmul_t(const double* x, const double* y, double* out) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) fmac_col<N>(out, y[j], x[j]);
+}
+
+// Column r of the group's N x N matrix whose row r is this lane's `row`,
+// through the LDS matrix `buf` (stride S).
+template <int N, int S>
+__device__ __forceinline__ void lds_transpose(double* buf, const double (&row)[N], int r, int rc, double (&col)[N]) {
+  if (r < N) st_row<N, S>(buf, r, row);
+  wave_sync();
+#pragma unroll
+  for (int l = 0; l < N; ++l) col[l] = buf[l * S + rc];
+  wave_sync();
+}
+
+#ifndef QT_DARE_ROW_WAVES
+#define QT_DARE_ROW_WAVES 2  // minimum waves per SIMD the row kernel's register allocation must allow
+#endif
+
+template <int N, int PP>
+struct RowDims {
+  static constexpr int GS = 16;
+  static constexpr int kProblemsPerWave = 4;
+  static constexpr int S = (N + 1) & ~1;
+  static constexpr int MAT = N * S;
+  static constexpr int RAW = 4 * MAT;  // H (the gain phase's P), A, Y, T
+  static constexpr int PROB = RAW + ((8 - RAW % 32) + 32) % 32;
+  static_assert(PP + N <= MAT && N <= GS && PP <= GS, "row layout");
+};
+
+template <int N, int PP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_WAVES, 8))) void dare_row_kernel(
+    int n, int p, int64_t m, const double* __restrict__ Ain, const double* __restrict__ Bin, int ab_per_problem,
+    double dt, double gravity, const double* __restrict__ mass, const double* __restrict__ q,
+    const double* __restrict__ rin, int fallback, double* K, double* P, int8_t* status, int32_t* iters) {
+  using D = RowDims<N, PP>;
+  constexpr int GS = D::GS, S = D::S;
+  __shared__ __attribute__((aligned(16))) double lds[D::kProblemsPerWave * D::PROB];
+  const int lane = threadIdx.x & 63, g = lane / GS, r = lane % GS;
+  const int rc = r < N ? r : N - 1, rp = r < PP ? r : PP - 1;
+  const int64_t pb = (int64_t)blockIdx.x * D::kProblemsPerWave + g;
+  const bool valid = pb < m;  // uniform over the group
+  double* Hl = lds + g * D::PROB;
+  double* Al = Hl + D::MAT;
+  double* Yl = Al + D::MAT;
+  double* Tl = Yl + D::MAT;
+  const bool hover = Ain == nullptr;
+  const double mss = (valid && mass) ? mass[pb] : 1.0;
+  const int64_t abm = ab_per_problem ? m : 1, abj = ab_per_problem ? pb : 0;
+  const bool real = valid && r < n;
+
+  auto a_in = [&](int j) -> double {
+    if (!(real && j < n)) return 0.0;
+    if (!hover) return Ain[(int64_t)(r * n + j) * abm + abj];
+    double a = (r == j) ? 1.0 : 0.0;
+    if (r < 3 && j == r + 3) a = dt;             // A_d = I + A_c dt (riccati_lqr.py:260)
+    if (n == 9 && r >= 6 && j == r - 6) a = dt;  // integral rows (308)
+    return a;
+  };
+  auto b_in = [&](int c) -> double {
+    if (!(real && c < p)) return 0.0;
+    if (!hover) return Bin[(int64_t)(r * p + c) * abm + abj];
+    if (r == 5 && c == 0) return 1.0 / mss * dt;  // riccati_lqr.py:250,261
+    if (r == 4 && c == 1) return -gravity * dt;   // 252
+    if (r == 3 && c == 2) return gravity * dt;    // 254
+    return 0.0;
+  };
+  auto r_in = [&](int c) -> double {
+    return (valid && r < p && c < p) ? rin[(int64_t)(r * p + c) * m + pb] : (r == c ? 1.0 : 0.0);
+  };
+
+  // ---- validation (riccati_lqr.py:57-116), as in dare_group_kernel
+  double hr[N];  // H = Q to start
+#pragma unroll
+  for (int j = 0; j < N; ++j) hr[j] = (real && j < n) ? q[(int64_t)(r * n + j) * m + pb] : 0.0;
+  int st = QT_DARE_OK;
+  {
+    bool qok = group_symmetric<N, S, GS>(hr, r, Tl);
+    double c[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) c[j] = hr[j] + ((r == j) ? 1e-10 : 0.0);
+    qok = group_cholesky_pd<N, GS>(c, r, Tl) && qok;
+    double rr[PP];
+#pragma unroll
+    for (int j = 0; j < PP; ++j) rr[j] = r_in(j);
+    bool rok = group_symmetric<PP, S, GS>(rr, r, Tl);
+#pragma unroll
+    for (int j = 0; j < PP; ++j) rr[j] -= (r == j) ? 1e-10 : 0.0;
+    rok = group_cholesky_pd<PP, GS>(rr, r, Tl) && rok;
+    st = !qok ? QT_DARE_Q_NOT_PSD : (!rok ? QT_DARE_R_NOT_PD : QT_DARE_OK);
+  }
+
+  // ---- G = B R^-1 B' (as in dare_group_kernel)
+  double gr[N];
+  int it = 0;
+  bool conv = false;
+  {
+    double br[PP];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) br[c] = b_in(c);
+    if (r < N) st_row<PP, S>(Yl, r, br);
+    wave_sync();
+    double w[PP + N];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) w[c] = r_in(c);
+#pragma unroll
+    for (int j = 0; j < N; ++j) w[PP + j] = r < PP ? Yl[j * S + rp] : 0.0;
+    wave_sync();
+    int col;
+    const bool ok = group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col);
+    if (st == QT_DARE_OK && !ok) st = QT_DARE_SINGULAR;
+    if (col >= 0) st_row<N, S>(Yl, col, w + PP);
+    wave_sync();
+    row_times<PP, N, S>(br, Yl, gr);
+    wave_sync();
+  }
+  double ar[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) ar[j] = a_in(j);
+
+  // ---- doublings: W = I + G H ; Winv = W^-1 ; Y1 = Winv A ; Y2 = Winv G ;
+  // H += sym(A' H Y1) ; G += sym(A Y2 A') ; A = A Y1, until |dH|_F <= tol |H|_F
+  while (true) {
+    const bool act = valid && st == QT_DARE_OK && !conv && it < kMaxIter;  // uniform over the group
+    if (__ballot(act) == 0) break;
+    if (!act) continue;
+    ++it;
+    double wi[N];
+    {
+      double w[N];
+      int col, pk[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) w[j] = j == r ? 1.0 : 0.0;
+      bmul_acc<N>(gr, hr, w);  // W = I + G H
+      if (!group_gj_invert<N, GS>(w, r, Tl, pk, &col)) {
+        st = QT_DARE_SINGULAR;
+        continue;
+      }
+      // W^-1[a][pk[k]] = S[pk[a]][k]: lane pk[a] (col = a) scatters its row to row a
+      if (col >= 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) Tl[col * S + pk[k]] = w[k];
+      }
+      wave_sync();
+#pragma unroll
+      for (int j = 0; j < N; ++j) wi[j] = Tl[rc * S + j];
+      wave_sync();
+    }
+    // Y2 = Winv G ; Y1 = Winv A ; T2 = Y2 A' ; T = H Y1 ; A_next = A Y1
+    double y1[N], y2[N], t[N], t2[N], an[N], u[N];
+    bmul<N>(wi, gr, y2);
+    bmul<N>(wi, ar, y1);
+    bmul_t<N>(y2, ar, t2);
+    bmul<N>(hr, y1, t);
+    bmul<N>(ar, y1, an);
+    // M = A' T ; H' = H + (M + M') / 2
+    lds_transpose<N, S>(Al, ar, r, rc, u);  // column r of A
+    double mm[N];
+    bmul<N>(u, t, mm);
+    lds_transpose<N, S>(Tl, mm, r, rc, u);
+    double dn = 0.0, hn = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double hnew = hr[j] + 0.5 * (mm[j] + u[j]);
+      dn += (hnew - hr[j]) * (hnew - hr[j]);
+      hn += hnew * hnew;
+      hr[j] = hnew;
+    }
+    dn = group_sum<GS>(r < N ? dn : 0.0);
+    hn = group_sum<GS>(r < N ? hn : 0.0);
+    const int flag = !isfinite(hn) ? -1 : (sqrt(dn) <= kTol * sqrt(hn) ? 1 : 0);
+    // M = A T2 ; G' = G + (M + M') / 2
+    bmul<N>(ar, t2, mm);
+    lds_transpose<N, S>(Yl, mm, r, rc, u);
+#pragma unroll
+    for (int j = 0; j < N; ++j) gr[j] += 0.5 * (mm[j] + u[j]), ar[j] = an[j];
+    if (flag < 0) st = QT_DARE_NO_CONVERGE;
+    if (flag == 1) conv = true;
+  }
+  if (valid && st == QT_DARE_OK && !conv) st = QT_DARE_NO_CONVERGE;
+  if (r < N) st_row<N, S>(Hl, r, hr);  // P for the gain phase and the output
+  wave_sync();
+
+  // ---- K = (R + B'PB)^-1 B'PA (riccati_lqr.py:181-182), as in dare_group_kernel
+  if (valid && st == QT_DARE_OK) {
+    if (r < N) {
+      double br[PP], a0[N];
+#pragma unroll
+      for (int c = 0; c < PP; ++c) br[c] = b_in(c);
+#pragma unroll
+      for (int j = 0; j < N; ++j) a0[j] = a_in(j);
+      st_row<PP, S>(Yl, r, br);
+      st_row<N, S>(Al, r, a0);
+    }
+    wave_sync();
+    double bc[N], tr[N];
+#pragma unroll
+    for (int l = 0; l < N; ++l) bc[l] = Yl[l * S + rp];
+    row_times<N, N, S>(bc, Hl, tr);
+    double w[PP + N];
+#pragma unroll
+    for (int c = 0; c < PP; ++c) {
+      double s = r_in(c);
+#pragma unroll
+      for (int l = 0; l < N; ++l) s += tr[l] * Yl[l * S + c];
+      w[c] = s;
+    }
+    row_times<N, N, S>(tr, Al, w + PP);
+    wave_sync();
+    int col;
+    if (!group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col)) st = QT_DARE_SINGULAR;
+    if (st == QT_DARE_OK && col >= 0 && col < p) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < n) K[(int64_t)(col * n + j) * m + pb] = w[PP + j];
+    }
+  }
+  if (!valid) return;
+  const bool ok = st == QT_DARE_OK;
+  if (P && r < n) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < n) P[(int64_t)(r * n + j) * m + pb] = ok ? Hl[r * S + j] : 0.0;
+  }
+  if (!ok && r < p) {
+    // a failed problem: zero gains, or the heuristic ones (riccati_lqr.py:756-774,
+    // controllers/__init__.py:537-572), each row written by its own lane:
+    // row 0 (thrust) from the z axis, row 1 (roll) from -y, row 2 (pitch) from x
+    int c0 = -1;
+    double kp = 0.0, kv = 0.0;
+    if (fallback && hover && r < 3) {
+      auto qd = [&](int i) { return q[(int64_t)(i * n + i) * m + pb]; };
+      auto rd = [&](int i) { return rin[(int64_t)(i * p + i) * m + pb]; };
+      const double rrate = (rd(1) + rd(2) + rd(3)) / 3.0;
+      const int ax = 2 - r;
+      heuristic_axis(qd(ax), qd(3 + ax), r == 0 ? rd(0) : rrate, kp, kv);
+      if (r == 1) kp = -kp, kv = -kv;
+      c0 = ax;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < n) K[(int64_t)(r * n + j) * m + pb] = j == c0 ? kp : (c0 >= 0 && j == c0 + 3 ? kv : 0.0);
+  }
+  if (r == 0) {
+    status[pb] = (int8_t)st;
+    if (iters) iters[pb] = it;
+  }
+}
+
+#ifndef QT_DARE_KERNEL
+#define QT_DARE_KERNEL 1  // 1: dare_row_kernel (DPP products), 0: dare_group_kernel (LDS products)
+#endif
+
+// Launch the dense kernel sized for (n, p): 6 / 4, 9 / 4, else 16 / 8.
 inline void launch_dare_group(int n, int p, int64_t m, const double* A, const double* B, int ab_per_problem,
                               double dt, double gravity, const double* mass, const double* q, const double* r,
                               int fallback, double* K, double* P, int8_t* status, int32_t* iters, hipStream_t s) {
+  if (QT_DARE_KERNEL == 1) {
+    const int grid = (int)((m + 3) / 4);
+    if (n <= 6 && p <= 4)
+      dare_row_kernel<6, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K,
+                                                P, status, iters);
+    else if (n <= 9 && p <= 4)
+      dare_row_kernel<9, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K,
+                                                P, status, iters);
+    else
+      dare_row_kernel<16, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback,
+                                                 K, P, status, iters);
+    return;
+  }
   if (n <= 6 && p <= 4) {
     const int grid = (int)((m + 7) / 8);
     dare_group_kernel<6, 4, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,

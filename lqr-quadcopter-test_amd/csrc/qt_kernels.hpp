@@ -132,6 +132,13 @@ __device__ __forceinline__ int wave_motion(const BatchDev& b, int64_t p) {
   return -1;
 }
 
+// The motion of the wave-aligned group holding `slot` (b.nseg > 0).
+__device__ __forceinline__ int slot_motion(const BatchDev& b, int64_t slot) {
+  for (int i = 0; i < b.nseg; ++i)
+    if (slot < b.seg_end[i]) return b.seg_motion[i];
+  return -1;
+}
+
 // The lane's feed-forward parameters: per episode (qt_batch.ff rows: velocity
 // gain xyz, acceleration gain xyz, velocity clamp) or the controller's.
 __device__ __forceinline__ FFLane ff_of(const BatchDev& b, const qt_ctrl_params& c, int64_t ep) {
@@ -844,6 +851,11 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
 #pragma unroll
     for (int i = 0; i < NI; ++i) st.integ[i * n + ep] = integ[i];
+    // a fresh pass without integral rows (KC 6) stores the zeros qt_reset would
+    if (FRESH && NI == 0 && lc.fresh_off && st.integ) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) st.integ[i * n + ep] = 0.0;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       st.target[i * n + ep] = tg.p[i];
@@ -866,6 +878,11 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
                   (!FF || (all_finite(fl.vg, 3) && all_finite(fl.ag, 3) && !(fl.vmax < 0.0))) &&
                   finite_bits(pl.inv_mass) && finite_bits(t) && fabs(t) < 1e300);
   for (int i = 9; i < 12; ++i) lane_ok = lane_ok && fabs(x[i]) <= e.max_angular_velocity;
+  // the grouped launch runs each wave's loop for its group's seg_motion and
+  // leaves a wave holding a lane whose own motion differs (a caller's
+  // inconsistent seg_motion, rollout_grouped_kernel) to this exact pass, which
+  // reads the motion per lane
+  if (FLAVOR == kExact && b.nseg && b.motion) lane_ok = lane_ok && (int)b.motion[ep] == slot_motion(b, slot);
   // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
   // never command yaw: a yaw at rest stays exactly zero
   // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
@@ -950,7 +967,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t slot = slot_at(b, p);
   if (slot < 0) return;
-  switch (wave_motion(b, p)) {
+  const int wm = wave_motion(b, p);
+  if (b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
+    // a lane's own motion is not its group's: the exact pass runs the wave
+    if (lc.defer_flag) *lc.defer_flag = lc.epoch;
+    return;
+  }
+  switch (wm) {
     case QT_MOTION_STATIONARY:
       rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;

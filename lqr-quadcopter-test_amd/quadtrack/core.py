@@ -81,6 +81,7 @@ class EpisodeBatch:
         `unpermute`."""
         if self.order is None or self.groups is None:
             raise ValueError("physical_groups needs a grouped batch (order and groups)")
+        validate(self)  # the gather below trusts `order`: a permutation of 0..n-1, checked first
         perm = self.order.to(torch.int64)
         col = lambda t: None if t is None else t.index_select(-1, perm).contiguous()  # noqa: E731
         K = self.K if self.K.shape[1] == 1 else col(self.K)

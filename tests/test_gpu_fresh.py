@@ -22,7 +22,7 @@ def qt():
     return quadtrack
 
 
-def _both(ctl, env_cfg, n, nsteps, motion=None, plant_mass=None, poison=None):
+def _both(ctl, env_cfg, n, nsteps, motion=None, plant_mass=None, poison=None, dirty=False):
     from quadtrack import core
     from quadtrack.env.config import EnvConfig
     from quadtrack.rollout import build_batch
@@ -38,6 +38,9 @@ def _both(ctl, env_cfg, n, nsteps, motion=None, plant_mass=None, poison=None):
     out = []
     for fresh in (True, False):
         st = core.RolloutState.empty(n, batch.device)
+        if dirty:  # a reused state buffer: every row holds an old value first
+            for t in (st.x, st.integ, st.t, st.acc, st.target):
+                t.fill_(7.0)
         if fresh:
             met = core.rollout_fresh(env, ctl.ctrl, crit, batch, st, nsteps)
         else:
@@ -71,6 +74,17 @@ def test_fresh_pass_bitwise(qt, case, nsteps):
     _, env_cfg, ctl_cfg = case
     met = _both(BatchedRiccatiLQR(ctl_cfg), env_cfg, 300, nsteps)
     assert np.all(met[-1] > 0)  # every episode stepped
+
+
+def test_fresh_pass_reused_state_buffer(qt):
+    """A fresh pass into a state buffer holding old values stores what
+    qt_reset -> qt_rollout would (the integral rows of an LQR pass included)."""
+    from quadtrack.controllers import BatchedPID, BatchedRiccatiLQR
+
+    _both(BatchedRiccatiLQR({"dt": 0.01}), {"target": {"motion_type": "linear"}}, 300, 777, dirty=True)
+    _both(BatchedRiccatiLQR({"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]}),
+          {"target": {"motion_type": "sinusoidal"}}, 300, 777, dirty=True)
+    _both(BatchedPID({"dt": 0.01}), {"target": {"motion_type": "circular"}}, 200, 777, dirty=True)
 
 
 def test_fresh_pass_pid_and_dense(qt):

@@ -5,11 +5,16 @@ condition into the horizons — low speed clamps, close position bounds, odd
 episode lengths, other time steps and rate limits, light and heavy plants,
 LQR / LQI / PID.  Decisions (steps, termination codes, counts) must be
 identical, values within 1e-9 (the two paths contract FMAs differently).
-GPU only."""
+Both are also checked against the oracle (oracle/qt_oracle.c, the reference's
+step restated) run on the same limits, masses, seeds and controller: step
+counts and termination codes exact, every other metric and the final state
+within 1e-5 absolute / 1e-8 relative (north star; reference
+quadcopter_env.py:428-465 termination, 513-535 constraints).  GPU only."""
 
 import numpy as np
 import pytest
 
+import oracle as O
 from test_gpu_parity import FIELDS
 
 pytestmark = pytest.mark.gpu
@@ -57,3 +62,28 @@ def test_horizon_randomised_limits(qt, i):
         else:
             np.testing.assert_allclose(mf[k], me[k], rtol=1e-9, atol=1e-9, err_msg=f)
     np.testing.assert_allclose(fast.state.x.cpu().numpy(), exact.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    # the oracle on the same limit set
+    om, oxf = _oracle(env, kind, ctl_cfg, mass, n)
+    for k, f in enumerate(FIELDS):
+        if f in ("termination_code", "steps"):
+            np.testing.assert_array_equal(mf[k], om[:, k], err_msg=f)
+        else:
+            np.testing.assert_allclose(mf[k], om[:, k], rtol=1e-8, atol=1e-5, err_msg=f)
+    np.testing.assert_allclose(fast.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=1e-5)
+
+
+def _oracle(env_cfg, kind, ctl_cfg, mass, n):
+    """The oracle's rollout of _config's episodes: per-episode plant mass, the
+    controller's own hover thrust (its mass stays 1 kg), seeds 0..n-1."""
+    cfg = dict(ctl_cfg)
+    if kind == "lqi":  # batched_controller("lqi"): use_lqi with its default q_int
+        cfg.update(use_lqi=True, q_int=[0.01, 0.01, 0.1])
+    elif kind == "pid":
+        cfg["controller"] = "pid"
+    c, K, kc, fb, _ = O.controller(cfg)
+    assert not fb
+    e = O.env_params(env_cfg)
+    pat, off = O.draws(int(e.motion), range(n))
+    x0 = np.array([O.initial_state(e, int(e.motion), pat[i], off[i]) for i in range(n)])
+    met, xf, _, _ = O.rollout(e, c, O.criteria(), None, pat, mass, None, K, kc, False, x0)
+    return met, xf

@@ -510,6 +510,31 @@ def test_mixed_motion_order_permutation(qt):
     np.testing.assert_allclose(a.state.x.cpu().numpy(), g.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
 
 
+def test_grouped_seg_motion_mismatch_runs_exact(qt):
+    """qt_rollout_grouped with seg_motion labels that disagree with
+    batch.motion (two groups' labels swapped): the grouped kernel leaves those
+    waves to the exact pass, which takes each episode's motion from
+    batch.motion, so the results are still those of the per-lane-motion run."""
+    import dataclasses
+
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch, run_closed_loop
+
+    n = 1000
+    motion = [i % 5 for i in range(n)]
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    plain = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, group_motion=False)
+    a = run_closed_loop(ctl, {}, n=n, batch=plain, max_steps=400)
+    g = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion)
+    sm, se = g.groups
+    sm = list(sm)
+    sm[1], sm[2] = sm[2], sm[1]
+    bad = dataclasses.replace(g, groups=(sm, list(se)))
+    r = run_closed_loop(ctl, {}, n=n, batch=bad, max_steps=400)
+    np.testing.assert_allclose(a.metrics.cpu().numpy(), r.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(a.state.x.cpu().numpy(), r.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
+
+
 # -------------------------------------------------------------------- DARE
 
 

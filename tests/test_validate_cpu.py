@@ -28,3 +28,14 @@ def test_order_permutation_accepted():
 def test_order_rejected(order, msg):
     with pytest.raises(ValueError, match=msg):
         core.validate(_batch(3, order))
+
+
+@pytest.mark.parametrize("order,msg", [([0, 1, 7], "out of range"), ([0, 0, 2], "permutation")])
+def test_physical_groups_checks_order(order, msg):
+    """A grouped batch is gathered through `order` before any launch: a bad
+    order is refused there too (not a device-side index_select assert)."""
+    b = _batch(3, order)
+    b.groups = (torch.tensor([0], dtype=torch.int32), torch.tensor([3], dtype=torch.int64))
+    b.motion = torch.zeros(3, dtype=torch.int8)
+    with pytest.raises(ValueError, match=msg):
+        b.physical_groups()
