@@ -443,9 +443,20 @@ QT_HD void rk4_linear(double lam, double h, double y, const double* f, double* o
   o[4] = h / 6.0 * (y + 2.0 * y2 + 2.0 * y3 + y4);
 }
 
+// The Euler step (_euler_step, quadcopter_env.py:319-327: x + dt f(x, u)) in
+// the same closed form: one stage at the step-start attitude, so
+// w_new = (1 - h lam) w + 10 h u, a_new = a + h w, v_new = (1 - h delta) v
+// + h acc_1, p_new = p + h v; no stage offsets (d2 = d3 = e3 = 0) and the
+// fourth "stage" offset d4 = h w is the whole attitude step, so that
+// attitude_trig_resid rotates the carried trig by the step's rounding only.
 QT_HD RateLin make_rate_lin(const qt_env_params& e) {
   RateLin L;
   const double h = e.dt, lam = 10.0 + e.drag_angular;
+  if (e.integrator == 1) {
+    L.wy = 1.0 - h * lam, L.wu = 10.0 * h, L.ay = h, L.au = 0.0;
+    L.h2 = 0.0, L.d3y = 0.0, L.d3u = 0.0, L.e3y = 0.0, L.d4y = h, L.d4u = 0.0;
+    return L;
+  }
   const double zero[4] = {0.0, 0.0, 0.0, 0.0}, ten[4] = {10.0, 10.0, 10.0, 10.0};
   double o[5];
   rk4_linear(lam, h, 1.0, zero, o);
@@ -460,6 +471,13 @@ QT_HD RateLin make_rate_lin(const qt_env_params& e) {
 QT_HD VelLin make_vel_lin(const qt_env_params& e, const Plant& pl) {
   VelLin L;
   const double h = e.dt, delta = e.drag_linear * pl.inv_mass;
+  if (e.integrator == 1) {  // Euler (make_rate_lin)
+    L.cv = 1.0 - h * delta, L.pv = h;
+    L.wv[0] = h, L.wv[1] = L.wv[2] = L.wv[3] = 0.0;
+    L.pa[0] = L.pa[1] = L.pa[2] = 0.0;
+    L.gv = pl.gz * pl.inv_mass * h, L.gp = 0.0;
+    return L;
+  }
   const double zero[4] = {0.0, 0.0, 0.0, 0.0};
   double o[5];
   rk4_linear(delta, h, 1.0, zero, o);
@@ -885,6 +903,16 @@ __host__ __device__ inline double stage3_residual_bound(const qt_env_params& e, 
 __host__ __device__ inline double attitude_residual_bound(const qt_env_params& e, const qt_ctrl_params& c) {
   const double lam = 10.0 + e.drag_angular, h = e.dt, k1 = (10.0 + lam) * c.max_rate;
   return h * h * h * lam * (1.0 + 0.5 * lam * h) / 12.0 * k1 * (1.0 + 1e-6) + 1e-15;  // + the wrap's rounding
+}
+
+// The yaw-at-rest flavour for the Euler integrator (make_rate_lin): the
+// controller clamps inside the env's (parsing is the identity) and the rate
+// bound below; the RK4 stage-offset bound does not apply (no stages).
+__host__ __device__ inline bool rate_bounded_ok(const qt_env_params& e, const qt_ctrl_params& c);
+__host__ __device__ inline bool euler_yaw0_ok(const qt_env_params& e, const qt_ctrl_params& c) {
+  return e.integrator == 1 && c.min_thrust >= e.min_thrust && c.max_thrust <= e.max_thrust &&
+         c.min_thrust <= c.max_thrust && c.max_rate <= e.max_angular_rate && c.max_rate >= 0.0 &&
+         e.max_angular_velocity >= 0.0 && rate_bounded_ok(e, c);
 }
 
 __host__ __device__ inline bool rate_bounded_ok(const qt_env_params& e, const qt_ctrl_params& c) {

@@ -897,6 +897,13 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
       if (FRESH && lc.fresh_off) store_state();  // the reset state, for the exact pass (launched without fresh_off)
       return;
     }
+    // qt_rollout_rewards on a fast flavour: the loop's pre-step tracking errors
+    // telescope into the env's post-step ones (post_k = pre_(k+1): positions
+    // are not constrained), so this launch's reward sum is
+    // -(dsum_e - pre_first + post_last).  The launch-start terms go to memory
+    // at once (nothing stays live across the loop).
+    const bool rw = FRESH && lc.reward && a.term == QT_TERM_RUNNING;
+    if (rw) lc.reward[ep] += a.sum_e + sqrt_pos(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
 #if QT_CLOCK_STAMP && defined(QT_FAST_TU)
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -916,6 +923,11 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
       g_qt_stamps[wave][5] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);
     }
 #endif
+    if (rw) {
+      const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
+      lc.reward[ep] -= a.sum_e + sqrt_pos(sq3_ref(q0, q1, q2));
+      lc.reward[n + ep] = sqrt(dot3_blas(q0, q1, q2));  // float(np.linalg.norm(...)), as the exact step
+    }
   } else {
     if (deferred != kExact && wave_ok) return;
     run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec, n,

@@ -586,6 +586,8 @@ unsigned long long* defer_flag_for(hipStream_t s) {
 int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
   if (fast && (ks || kc == 3 || no_yaw) && rate_bounded_ok(e, c)) return kYaw0;
+  // Euler: the yaw-at-rest closed form only (make_rate_lin), no staged fast step
+  if (QT_ABLATE == 0 && rec == nullptr && (ks || kc == 3 || no_yaw) && euler_yaw0_ok(e, c)) return kYaw0;
   return fast ? kFast : kExact;
 }
 
@@ -604,8 +606,9 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
   lc.fresh_off = fresh_off, lc.met = met;  // qt_rollout_fresh: reset in the prologue, metrics in the epilogue
   const bool ks_eff = ks || kc == 3;
   const bool uni = !b.plant_mass && !b.hover && !b.k_per_episode;
-  // rewards are accumulated by the exact step only
-  const int flavor = reward ? kExact : flavor_for(kc, ks, no_yaw, e, c, rec);
+  // rewards: the exact step accumulates them per step, a fast flavour from its
+  // tracking-error sums (rollout_lane)
+  const int flavor = flavor_for(kc, ks, no_yaw, e, c, rec);
   if (flavor != kExact) {
     lc.defer_flag = defer_flag_for(s);  // null (no flag: the exact pass tests every wave) if unavailable
     lc.epoch = g_defer_epoch.fetch_add(1, std::memory_order_relaxed) + 1;

@@ -61,3 +61,44 @@ def test_evaluate_epoch_means_are_numpy_means():
         assert r.mean_reward == float(np.mean(r.episode_reward.cpu().numpy()))
         assert r.mean_on_target_ratio == float(np.mean(r.episode_on_target_ratio.cpu().numpy()))
         assert r.mean_tracking_error == float(np.mean(r.episode_tracking_error.cpu().numpy()))
+
+
+@pytest.mark.parametrize("controller,motion", [("riccati_lqr", "circular"), ("lqi", "sinusoidal"),
+                                               ("pid", "linear"), ("lqr", "figure8")])
+def test_rewards_fast_flavour_matches_exact(controller, motion):
+    """qt_rollout_rewards on the yaw-at-rest fast flavour (rewards telescoped
+    from its pre-step tracking-error sums) against the exact step, which
+    accumulates -(post-step error) per step.  The exact run starts every
+    episode with a 1e-300 rad/s yaw rate: no lane then passes the yaw-at-rest
+    wave test, every wave goes to the exact pass, and the trajectories differ
+    by ~1e-300.  Reward sums and last errors within 1e-9, step counts and
+    on-target counts exact — in one launch and in three uneven chunks."""
+    import torch
+
+    from quadtrack import _abi, core
+    from quadtrack.controllers import batched_controller
+    from quadtrack.rollout import build_batch
+    from quadtrack.train import env_config_for
+
+    dev = _abi.require_gpu()
+    cfg = env_config_for(7, motion, 12.0)
+    env = cfg.to_params()
+    n = 300
+    ctl = batched_controller(controller, {}, device=dev)
+    batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+    out = []
+    for exact, chunks in ((False, [1200]), (False, [401, 555, 244]), (True, [1200])):
+        st = core.RolloutState.empty(n, dev)
+        core.reset(env, batch, st)
+        if exact:
+            st.x[11] = 1e-300
+        reward = torch.zeros(2, n, dtype=torch.float64, device=dev)
+        for k in chunks:
+            core.rollout_rewards(env, ctl.ctrl, core.criteria(), batch, st, k, reward)
+        out.append((reward.cpu().numpy(), st.acc.cpu().numpy()))
+    (r0, a0), (r1, a1), (re, ae) = out
+    assert np.all(ae[_abi.ACC_STEPS] > 0)
+    for r, a in ((r0, a0), (r1, a1)):
+        np.testing.assert_array_equal(a[_abi.ACC_STEPS], ae[_abi.ACC_STEPS])
+        np.testing.assert_array_equal(a[_abi.ACC_ON_POST], ae[_abi.ACC_ON_POST])
+        np.testing.assert_allclose(r, re, rtol=1e-9, atol=1e-9)
