@@ -6,12 +6,14 @@ reference).
 Workload (BASELINE.json configs[1]): per GPU 65,536
 independent 30 s episodes (3,000 steps at dt = 0.01), linear target,
 Riccati-LQR with the default weights (one shared DARE gain), seeds = global
-episode index.  One bench "step" = one full pass of the hot path over the
-batch: reset kernel (inputs already in HBM) -> fused closed-loop rollout
-kernel (3,000 steps of compute_action -> env.step with fused metric
-accumulation) -> per-episode metrics kernel -> summary partials (+ one RCCL
-all-reduce of the metric vector when N > 1).  value = all ranks' env-steps /
-max-over-ranks wall time.
+episode index.  One bench "step" = one full evaluation pass over the batch,
+inputs already in HBM: the fresh launch (qt_rollout_fresh: the fused
+closed-loop rollout kernel forms the reset state in its prologue, runs the
+3,000 steps of compute_action -> env.step with fused metric accumulation and
+writes the per-episode metric rows in its epilogue), the exact-pass launch
+after it (returns at once when no wave was deferred), then the summary's two
+launches (partials, + one async RCCL all-reduce of the sums when N > 1).
+value = all ranks' env-steps / max-over-ranks wall time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 runs one process per GPU under torch.distributed.run: when WORLD_SIZE is
@@ -43,6 +45,10 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, spec (half the FP32 vector 157
 HBM_PEAK_GBS = 8000.0
 # the dominant kernel of the bench workload: yaw-at-rest fast flavour, linear target, 6-column structured K
 KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true"
+# The committed rocprofv3 session this line reads its profile, traffic and
+# issued-FP64 numbers from (scripts/profile_session.sh's condensed CSVs):
+# one named directory, never "the newest".  --profile-dir overrides it.
+PROFILE_DIR = "profiles/r04"
 # Warm-up floor: a fresh box's first ~0.5 s of passes run at lower clocks
 # (round 2: --warmup 5, 8 ms of GPU work, measured ~7% below --warmup 20), so
 # the warm-up runs for at least this long whatever --warmup says.
@@ -62,6 +68,8 @@ def parse():
     ap.add_argument("--cpu-sample-1core", type=int, default=4096, help="episodes of the 1-thread CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the OpenMP CPU leg (0: see cpu_baseline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-dir", default=PROFILE_DIR,
+                    help="committed rocprofv3 summaries (kernel_stats.csv, pmc_*.csv) the line cites")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU plumbing check of the N-rank launch (gloo, no kernels): prints the ranks seen")
     return ap.parse_args()
@@ -306,13 +314,13 @@ def main():
     if rank == 0:
         achieved = FLOPS_PER_ENV_STEP * local_env_steps / (kern_ms * 1e-3) / 1e12
         # the dominant kernel: the fast yaw-at-rest flavour (older profiles: the single-flavour kernel)
-        traffic, traffic_src = pmc_traffic((KERNEL_TAG,))
+        traffic, traffic_src = pmc_traffic(args.profile_dir, KERNEL_TAG)
         # algorithmic HBM bytes of one fresh launch: per-episode pattern 3 and start offset 3 doubles
         # in; x 12, target 9, t, acc 14 and the 14 metric rows out; gains are a broadcast
         algo_bytes = (6 + 50) * 8 * n
         # the same frac from the committed rocprofv3 kernel trace (fast launch alone; its deferred
         # exact pass runs no wave at this workload)
-        prof = profiled_kernel((KERNEL_TAG,))
+        prof = profiled_kernel(args.profile_dir, KERNEL_TAG)
         prof_line = None
         if prof is not None:
             p_ms, p_min, p_calls, p_dir = prof
@@ -320,6 +328,16 @@ def main():
             prof_line = {"source": f"{p_dir}/kernel_stats.csv", "kernel_avg_ms": round(p_ms, 4),
                          "kernel_min_ms": round(p_min, 4), "calls": p_calls, "achieved": round(p_ach, 3),
                          "frac": round(p_ach / FP64_PEAK_TFLOPS, 4)}
+        # what the hardware issues: FP64 VALU instructions of the dominant kernel from the committed
+        # counter pass (64 lanes x (2 FMA + MUL + ADD + TRANS) per wave instruction), over this run's
+        # kernel time
+        issued = issued_fp64(args.profile_dir, KERNEL_TAG)
+        issued_line = None
+        if issued is not None:
+            i_flops, i_src, i_counts = issued
+            i_ach = i_flops / (kern_ms * 1e-3) / 1e12
+            issued_line = {"flops_per_launch": i_flops, "per_env_step": round(i_flops / local_env_steps, 2),
+                           "source": i_src, "counters_per_launch": i_counts}
         line = {
             "metric": "env-steps/sec at 65 536 parallel episodes per GPU (30 s @ dt=0.01, Riccati-LQR closed loop)",
             "value": round(value, 1),
@@ -351,6 +369,9 @@ def main():
                          "kernel_ms_min_median_max": [round(float(v), 4) for v in
                                                       (kern_all.min(), np.median(kern_all), kern_all.max())],
                          "flops_per_env_step": FLOPS_PER_ENV_STEP,
+                         "issued_tflops": None if issued is None else round(i_ach, 3),
+                         "issued_frac": None if issued is None else round(i_ach / FP64_PEAK_TFLOPS, 4),
+                         "issued": issued_line,
                          "profiled": prof_line},
             "ranks": {"world_size_seen": seen, "backend": "nccl (RCCL)" if world > 1 else None,
                       "env_steps_per_pass_per_rank": per_rank},
@@ -363,49 +384,60 @@ def main():
         dist.destroy_process_group()
 
 
-def profiled_kernel(kernel_tags):
-    """Average duration (ms) of the dominant kernel in the newest committed
-    rocprofv3 kernel trace (profiles/r*/kernel_stats.csv) whose kernel name
-    contains one of `kernel_tags`: (avg_ms, min_ms, calls, profile dir)."""
+def profiled_kernel(profile_dir, tag):
+    """Average duration (ms) of the dominant kernel (name containing `tag`) in
+    the committed rocprofv3 kernel trace <profile_dir>/kernel_stats.csv:
+    (avg_ms, min_ms, calls, profile dir), or None."""
     import csv
-    import glob
 
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats.csv")), reverse=True):
-        for tag in kernel_tags:
-            rows = [r for r in csv.DictReader(open(path)) if tag in r["Name"]]
-            if rows:
-                r = rows[0]
-                return (float(r["AverageNs"]) * 1e-6, float(r["MinNs"]) * 1e-6, int(r["Calls"]),
-                        os.path.relpath(os.path.dirname(path), ROOT))
-    return None
+    path = os.path.join(ROOT, profile_dir, "kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    rows = [r for r in csv.DictReader(open(path)) if tag in r["Name"]]
+    if not rows:
+        return None
+    r = rows[0]
+    return float(r["AverageNs"]) * 1e-6, float(r["MinNs"]) * 1e-6, int(r["Calls"]), profile_dir
 
 
-def pmc_traffic(kernel_tags):
+def _pmc_avg(path, counter, tag):
+    """Per-dispatch average of `counter` for the kernel named like `tag` in a
+    scripts/pmc_summary.py CSV, or None."""
+    import csv
+
+    if not os.path.exists(path):
+        return None
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter and tag in r["Kernel_Name"]]
+    return float(rows[0]["Average_Per_Dispatch"]) if rows else None
+
+
+def pmc_traffic(profile_dir, tag):
     """HBM bytes per rollout launch from the committed rocprofv3 PMC passes
-    (profiles/r*/pmc_FETCH_SIZE.csv, pmc_WRITE_SIZE.csv; scripts/profile_session.sh),
-    newest profile first, first kernel tag that matches.
+    (<profile_dir>/pmc_FETCH_SIZE.csv, pmc_WRITE_SIZE.csv; scripts/profile_session.sh).
     gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
     (MI355X_MICROARCH.md §HBM), so it is doubled; both counters are in KiB."""
-    import csv
-    import glob
+    f = _pmc_avg(os.path.join(ROOT, profile_dir, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", tag)
+    w = _pmc_avg(os.path.join(ROOT, profile_dir, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", tag)
+    if f is None or w is None:
+        return None, None
+    return (2.0 * f + w) * 1024.0, profile_dir
 
-    dirs = sorted((d for d in glob.glob(os.path.join(ROOT, "profiles", "r*"))
-                   if os.path.exists(os.path.join(d, "pmc_FETCH_SIZE.csv"))), reverse=True)
 
-    def avg(path, counter, tag):
-        rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter and tag in r["Kernel_Name"]]
-        if rows and "Average_Per_Dispatch" in rows[0]:  # scripts/pmc_summary.py form (round 3 on)
-            return float(rows[0]["Average_Per_Dispatch"])
-        vals = [float(r["Counter_Value"]) for r in rows]  # rocprofv3's per-dispatch rows
-        return sum(vals) / len(vals) if vals else None
+F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
 
-    for d in dirs:
-        for tag in kernel_tags:
-            f = avg(os.path.join(d, "pmc_FETCH_SIZE.csv"), "FETCH_SIZE", tag)
-            w = avg(os.path.join(d, "pmc_WRITE_SIZE.csv"), "WRITE_SIZE", tag)
-            if f is not None and w is not None:
-                return (2.0 * f + w) * 1024.0, os.path.relpath(d, ROOT)
-    return None, None
+
+def issued_fp64(profile_dir, tag):
+    """FP64 flops the hardware issues per launch of the kernel named like
+    `tag`, from the committed counter pass <profile_dir>/pmc_F64_summary.csv:
+    64 lanes x (2 FMA + MUL + ADD + TRANS) per wave instruction (every lane of
+    the bench's waves is active).  (flops, source, counts) or None."""
+    path = os.path.join(ROOT, profile_dir, "pmc_F64_summary.csv")
+    counts = {c: _pmc_avg(path, c, tag) for c in F64_COUNTERS}
+    if any(v is None for v in counts.values()):
+        return None
+    flops = 64.0 * (2.0 * counts["SQ_INSTS_VALU_FMA_F64"] + counts["SQ_INSTS_VALU_MUL_F64"]
+                    + counts["SQ_INSTS_VALU_ADD_F64"] + counts["SQ_INSTS_VALU_TRANS_F64"])
+    return flops, f"{profile_dir}/pmc_F64_summary.csv", counts
 
 
 def cpu_baseline(args, cfg, seeds, gpu_met):

@@ -853,9 +853,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVE
 // (row_newbcast: the DPP control gfx950 applies to 64-bit operands), N per
 // block.  Written as inline asm because the compiler does not fold a 64-bit
 // DPP move into the FMA (it would issue a v_mov_b64_dpp per product term).
-// Each block opens with s_nop 4: a DPP source VGPR written by the VALU needs
-// 2 wait states and an EXEC write 5, and the compiler's hazard recognizer
-// does not look inside inline asm.
+// Hazards: a DPP source VGPR written by the VALU needs 2 wait states before
+// the DPP read, an EXEC write 5, and the compiler's hazard recognizer does not
+// look inside inline asm.  The first block of a product (NOP) opens with
+// s_nop 4; the blocks after it follow the previous block's FMAs, which write
+// only accumulators.  tests/test_dare_asm.py checks the built kernels: no DPP
+// source written by a VALU instruction within 2 wait states and no EXEC write
+// within 5 before any v_fmac_f64_dpp, and no block entered from a branch
+// inside that window.
 #define QT_FR(i) "v_fmac_f64_dpp %[a" #i "], %[y" #i "], %[x] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
 #define QT_FC(i) "v_fmac_f64_dpp %[a" #i "], %[y], %[x] row_newbcast:" #i " row_mask:0xf bank_mask:0xf\n\t"
 #define QT_A(i) [a##i] "+v"(a[i])
@@ -873,35 +878,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVE
 #define QT_A16 QT_A9, QT_A(9), QT_A(10), QT_A(11), QT_A(12), QT_A(13), QT_A(14), QT_A(15)
 #define QT_Y16 QT_Y9, QT_Y(9), QT_Y(10), QT_Y(11), QT_Y(12), QT_Y(13), QT_Y(14), QT_Y(15)
 
+// one asm block, with or without the s_nop 4 in front (NOP)
+#define QT_BLOCK(NOP, BODY, OUTS, INS) \
+  do {                                  \
+    if constexpr (NOP)                  \
+      asm("s_nop 4\n\t" BODY : OUTS : INS); \
+    else                                \
+      asm(BODY : OUTS : INS);           \
+  } while (0)
+#define QT_COMMA ,
+
 // a[j] += Y[L][j] x for j < N, row L of Y in lane L's y
-template <int N, int L>
+template <int N, int L, bool NOP>
 __device__ __forceinline__ void fmac_row(double* a, const double* y, double x) {
   static_assert(N == 6 || N == 9 || N == 16, "row block sizes");
   if constexpr (N == 6)
-    asm("s_nop 4\n\t" QT_FR6 : QT_A6 : QT_Y6, [x] "v"(x), [l] "n"(L));
+    QT_BLOCK(NOP, QT_FR6, QT_A6, QT_Y6 QT_COMMA[x] "v"(x) QT_COMMA[l] "n"(L));
   else if constexpr (N == 9)
-    asm("s_nop 4\n\t" QT_FR9 : QT_A9 : QT_Y9, [x] "v"(x), [l] "n"(L));
+    QT_BLOCK(NOP, QT_FR9, QT_A9, QT_Y9 QT_COMMA[x] "v"(x) QT_COMMA[l] "n"(L));
   else
-    asm("s_nop 4\n\t" QT_FR16 : QT_A16 : QT_Y16, [x] "v"(x), [l] "n"(L));
+    QT_BLOCK(NOP, QT_FR16, QT_A16, QT_Y16 QT_COMMA[x] "v"(x) QT_COMMA[l] "n"(L));
 }
 
 // a[l] += Y[l][j] x for l < N, entry j of row l of Y in lane l's yj
-template <int N>
+template <int N, bool NOP>
 __device__ __forceinline__ void fmac_col(double* a, double yj, double x) {
   static_assert(N == 6 || N == 9 || N == 16, "column block sizes");
   if constexpr (N == 6)
-    asm("s_nop 4\n\t" QT_FC6 : QT_A6 : [y] "v"(yj), [x] "v"(x));
+    QT_BLOCK(NOP, QT_FC6, QT_A6, [y] "v"(yj) QT_COMMA[x] "v"(x));
   else if constexpr (N == 9)
-    asm("s_nop 4\n\t" QT_FC9 : QT_A9 : [y] "v"(yj), [x] "v"(x));
+    QT_BLOCK(NOP, QT_FC9, QT_A9, [y] "v"(yj) QT_COMMA[x] "v"(x));
   else
-    asm("s_nop 4\n\t" QT_FC16 : QT_A16 : [y] "v"(yj), [x] "v"(x));
+    QT_BLOCK(NOP, QT_FC16, QT_A16, [y] "v"(yj) QT_COMMA[x] "v"(x));
 }
 
 // acc[j] += sum_l x[l] Y[l][j] (l, j < N), row l of Y in lane l's y
 template <int N, int L = 0>
 __device__ __forceinline__ void bmul_acc(const double* x, const double* y, double* acc) {
   if constexpr (L < N) {
-    fmac_row<N, L>(acc, y, x[L]);
+    fmac_row<N, L, L == 0>(acc, y, x[L]);
     bmul_acc<N, L + 1>(x, y, acc);
   }
 }
@@ -915,12 +930,76 @@ __device__ __forceinline__ void bmul(const double* x, const double* y, double* o
 }
 
 // out = x Y' (out[l] = sum_j x[j] Y[l][j]), row l of Y in lane l's y
+template <int N, int J = 0>
+__device__ __forceinline__ void bmul_t_acc(const double* x, const double* y, double* out) {
+  if constexpr (J < N) {
+    fmac_col<N, J == 0>(out, y[J], x[J]);
+    bmul_t_acc<N, J + 1>(x, y, out);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void bmul_t(const double* x, const double* y, double* out) {
 #pragma unroll
   for (int j = 0; j < N; ++j) out[j] = 0.0;
+  bmul_t_acc<N>(x, y, out);
+}
+
+// Group maximum of a 32-bit unsigned key over the 16 lanes of a DPP row
+// (each step's DPP move fuses into v_max_u32).
+__device__ __forceinline__ unsigned row_max_u32(unsigned v) {
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor1, 0xf, 0xf, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor2, 0xf, 0xf, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppHalfMirror, 0xf, 0xf, false));
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppMirror, 0xf, 0xf, false));
+  return v;
+}
+
+// 1 / x to within an ulp or so (v_rcp_f64 and two Newton steps): x finite, nonzero
+__device__ __forceinline__ double recip_newton(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = fma(y, fma(-x, y, 1.0), y);
+  return fma(y, fma(-x, y, 1.0), y);
+}
+
+// group_gj_invert for the row kernel (one problem per 16-lane DPP row): the
+// pivot is the row whose |w[k]| has the largest high word (exponent and the
+// top 20 mantissa bits: partial pivoting to 2^-20, ties to the lowest row),
+// found by a 32-bit DPP maximum, and the pivot row is scaled by a Newton
+// reciprocal.  Same in-place form and return values as group_gj_invert.
+template <int NR>
+__device__ __forceinline__ bool row_gj_invert(double (&w)[NR], int r, double* piv, int (&pk)[NR], int* col) {
+  bool used = r >= NR;
+  *col = -1;
 #pragma unroll
-  for (int j = 0; j < N; ++j) fmac_col<N>(out, y[j], x[j]);
+  for (int k = 0; k < NR; ++k) {
+    const unsigned key = used ? 0u : ((unsigned)__double2hiint(w[k]) & 0x7fffffffu);
+    const unsigned mx = row_max_u32(key);
+    if (mx == 0u) return false;
+    const int p = __builtin_ctz(group_bits<16>(__ballot(!used && key == mx)));
+    pk[k] = p;
+    if (r == p) {
+      const double inv = recip_newton(w[k]);
+#pragma unroll
+      for (int j = 0; j < NR; ++j) w[j] = j == k ? inv : w[j] * inv;
+      st_row<NR, NR + (NR & 1)>(piv, 0, w);
+      used = true;
+      *col = k;
+    }
+    wave_sync();
+    if (r != p) {
+      const double f = w[k];
+#pragma unroll
+      for (int j = 0; j + 1 < NR; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(piv + j);
+        w[j] = j == k ? -f * v.x : w[j] - f * v.x;
+        w[j + 1] = j + 1 == k ? -f * v.y : w[j + 1] - f * v.y;
+      }
+      if (NR & 1) w[NR - 1] = NR - 1 == k ? -f * piv[NR - 1] : w[NR - 1] - f * piv[NR - 1];
+    }
+    wave_sync();
+  }
+  return true;
 }
 
 // Column r of the group's N x N matrix whose row r is this lane's `row`,
@@ -933,6 +1012,13 @@ __device__ __forceinline__ void lds_transpose(double* buf, const double (&row)[N
   for (int l = 0; l < N; ++l) col[l] = buf[l * S + rc];
   wave_sync();
 }
+
+// 1: symmetrise H and G after every doubling, (M + M') / 2, as dare_group_kernel
+// does; 0: add M as computed (A' (H W^-1) A and A (W^-1 G) A' are symmetric in
+// exact arithmetic: H W^-1 = (I + H G)^-1 H), which spares two LDS transposes
+#ifndef QT_DARE_SYM
+#define QT_DARE_SYM 1
+#endif
 
 #ifndef QT_DARE_ROW_WAVES
 #define QT_DARE_ROW_WAVES 2  // minimum waves per SIMD the row kernel's register allocation must allow
@@ -1053,7 +1139,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
 #pragma unroll
       for (int j = 0; j < N; ++j) w[j] = j == r ? 1.0 : 0.0;
       bmul_acc<N>(gr, hr, w);  // W = I + G H
-      if (!group_gj_invert<N, GS>(w, r, Tl, pk, &col)) {
+      if (!row_gj_invert<N>(w, r, Tl, pk, &col)) {
         st = QT_DARE_SINGULAR;
         continue;
       }
@@ -1074,27 +1160,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     bmul_t<N>(y2, ar, t2);
     bmul<N>(hr, y1, t);
     bmul<N>(ar, y1, an);
-    // M = A' T ; H' = H + (M + M') / 2
+    // M = A' T ; H' = H + M (QT_DARE_SYM: + (M + M') / 2)
     lds_transpose<N, S>(Al, ar, r, rc, u);  // column r of A
     double mm[N];
     bmul<N>(u, t, mm);
-    lds_transpose<N, S>(Tl, mm, r, rc, u);
     double dn = 0.0, hn = 0.0;
+    if (QT_DARE_SYM) {
+      lds_transpose<N, S>(Tl, mm, r, rc, u);
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const double hnew = hr[j] + 0.5 * (mm[j] + u[j]);
-      dn += (hnew - hr[j]) * (hnew - hr[j]);
-      hn += hnew * hnew;
-      hr[j] = hnew;
+      for (int j = 0; j < N; ++j) {
+        const double hnew = hr[j] + 0.5 * (mm[j] + u[j]);
+        dn += (hnew - hr[j]) * (hnew - hr[j]);
+        hn += hnew * hnew;
+        hr[j] = hnew;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        hr[j] += mm[j];
+        dn = fma(mm[j], mm[j], dn);
+        hn = fma(hr[j], hr[j], hn);
+      }
     }
     dn = group_sum<GS>(r < N ? dn : 0.0);
     hn = group_sum<GS>(r < N ? hn : 0.0);
-    const int flag = !isfinite(hn) ? -1 : (sqrt(dn) <= kTol * sqrt(hn) ? 1 : 0);
-    // M = A T2 ; G' = G + (M + M') / 2
-    bmul<N>(ar, t2, mm);
-    lds_transpose<N, S>(Yl, mm, r, rc, u);
+    // |dH|_F <= tol |H|_F, squared (tol^2 = 1e-28: no square roots)
+    const int flag = !isfinite(hn) ? -1 : (dn <= kTol * kTol * hn ? 1 : 0);
+    // M = A T2 ; G' = G + M (QT_DARE_SYM: + (M + M') / 2)
+    if (QT_DARE_SYM) {
+      bmul<N>(ar, t2, mm);
+      lds_transpose<N, S>(Yl, mm, r, rc, u);
 #pragma unroll
-    for (int j = 0; j < N; ++j) gr[j] += 0.5 * (mm[j] + u[j]), ar[j] = an[j];
+      for (int j = 0; j < N; ++j) gr[j] += 0.5 * (mm[j] + u[j]);
+    } else {
+      bmul_acc<N>(ar, t2, gr);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) ar[j] = an[j];
     if (flag < 0) st = QT_DARE_NO_CONVERGE;
     if (flag == 1) conv = true;
   }

@@ -109,3 +109,37 @@ def test_visible_gpu_count_without_hip():
     assert int(m) == min(int(n), 1)
     if not gpu_available():
         assert int(n) == 0
+
+
+def test_profile_readers_use_one_named_directory(tmp_path):
+    """bench.py cites the committed rocprofv3 summaries of ONE directory
+    (--profile-dir, default PROFILE_DIR): kernel average, HBM traffic and the
+    issued FP64 flops (64 x (2 FMA + MUL + ADD + TRANS) per launch) come from
+    that directory's files, and a directory without them gives None (never
+    another round's files)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    tag = bench.KERNEL_TAG
+    name = f"void qtk::{tag}, false>(args)"
+    d = tmp_path / "prof"
+    d.mkdir()
+    (d / "kernel_stats.csv").write_text('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs"\n'
+                                        f'"{name}",10,13000000,1300000.0,99.0,1290000,1310000\n')
+    hdr = "Kernel_Name,Counter_Name,Dispatches,Average_Per_Dispatch\n"
+    (d / "pmc_FETCH_SIZE.csv").write_text(hdr + f'"{name}",FETCH_SIZE,3,100.0\n')
+    (d / "pmc_WRITE_SIZE.csv").write_text(hdr + f'"{name}",WRITE_SIZE,3,50.0\n')
+    (d / "pmc_F64_summary.csv").write_text(hdr + "".join(
+        f'"{name}",{c},3,{v}\n' for c, v in zip(bench.F64_COUNTERS, (10.0, 4.0, 3.0, 1.0))))
+    rel = os.path.relpath(d, ROOT)
+    ms, mn, calls, src = bench.profiled_kernel(rel, tag)
+    assert (ms, mn, calls, src) == (1.3, 1.29, 10, rel)
+    assert bench.pmc_traffic(rel, tag) == ((2 * 100.0 + 50.0) * 1024.0, rel)
+    flops, src, counts = bench.issued_fp64(rel, tag)
+    assert flops == 64.0 * (2 * 10.0 + 4.0 + 3.0 + 1.0) and src == f"{rel}/pmc_F64_summary.csv"
+    empty = tmp_path / "none"
+    empty.mkdir()
+    rel2 = os.path.relpath(empty, ROOT)
+    assert bench.profiled_kernel(rel2, tag) is None
+    assert bench.pmc_traffic(rel2, tag) == (None, None)
+    assert bench.issued_fp64(rel2, tag) is None
