@@ -31,6 +31,8 @@ namespace {
 
 constexpr int kMaxIter = 64;
 constexpr double kTol = 1e-14;
+// largest |W (W^-1 1) - 1| the row kernel's inverse without row exchanges may leave
+constexpr double kInvCheck = 1e-10;
 
 // heuristic (double-integrator) gains, K row for one axis
 __device__ __forceinline__ void heuristic_axis(double qp, double qv, double r, double& kp, double& kv) {
@@ -945,6 +947,78 @@ __device__ __forceinline__ void bmul_t(const double* x, const double* y, double*
   bmul_t_acc<N>(x, y, out);
 }
 
+// 1 / x to within an ulp or so (v_rcp_f64 and two Newton steps): x finite, nonzero
+__device__ __forceinline__ double recip_newton(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = fma(y, fma(-x, y, 1.0), y);
+  return fma(y, fma(-x, y, 1.0), y);
+}
+
+// Lane L's value of each DPP row (row_newbcast), as inline asm with its own
+// s_nop 4 (the source was written by inline-asm FMAs just before, which the
+// compiler's hazard recognizer does not see)
+template <int L>
+__device__ __forceinline__ double row_bcast_asm(double v) {
+  double o;
+  asm("s_nop 4\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(o) : "v"(v), "n"(L));
+  return o;
+}
+
+// a[j] += A[K][j] x for j < N, row K of A in lane K's a: the elimination of
+// row K from every row in place (the DPP reads lane K's register before the
+// FMA writes the lane's own), one asm block so that nothing comes between its
+// FMAs
+#define QT_FS(i) "v_fmac_f64_dpp %[a" #i "], %[a" #i "], %[x] row_newbcast:%[l] row_mask:0xf bank_mask:0xf\n\t"
+#define QT_FS6 QT_FS(0) QT_FS(1) QT_FS(2) QT_FS(3) QT_FS(4) QT_FS(5)
+#define QT_FS9 QT_FS6 QT_FS(6) QT_FS(7) QT_FS(8)
+#define QT_FS16 QT_FS9 QT_FS(9) QT_FS(10) QT_FS(11) QT_FS(12) QT_FS(13) QT_FS(14) QT_FS(15)
+template <int N, int K>
+__device__ __forceinline__ void elim_row(double* a, double x) {
+  static_assert(N == 6 || N == 9 || N == 16, "row block sizes");
+  if constexpr (N == 6)
+    asm("s_nop 4\n\t" QT_FS6 : QT_A6 : [x] "v"(x), [l] "n"(K));
+  else if constexpr (N == 9)
+    asm("s_nop 4\n\t" QT_FS9 : QT_A9 : [x] "v"(x), [l] "n"(K));
+  else
+    asm("s_nop 4\n\t" QT_FS16 : QT_A16 : [x] "v"(x), [l] "n"(K));
+}
+
+// acc += sum_l Y[l] x[l] (l < N), Y[l] lane l's y: a dot product whose
+// right factor is spread over the row's lanes
+template <int N, int L = 0>
+__device__ __forceinline__ void dot_lanes(double& acc, double y, const double* x) {
+  if constexpr (L < N) {
+    if constexpr (L == 0)
+      asm("s_nop 4\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+          : "+v"(acc) : "v"(y), "v"(x[L]), "n"(L));
+    else
+      asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+          : "+v"(acc) : "v"(y), "v"(x[L]), "n"(L));
+    dot_lanes<N, L + 1>(acc, y, x);
+  }
+}
+
+// In-place Gauss-Jordan inversion of the group's N x N matrix W (row r in
+// this lane's w; lanes r >= N hold zero rows) WITHOUT pivoting: step k
+// eliminates with row k itself, broadcast from lane k by DPP (no LDS, no
+// branch).  Normalisation is deferred: row k stays scaled by its pivot p_k
+// through the later steps (every update is linear in it) and each lane
+// divides its row by its own pivot at the end.  Rows come out in natural
+// order.  The caller checks the result (W^-1 without pivoting can lose
+// accuracy on a matrix that needs row exchanges) and falls back to
+// row_gj_invert.
+template <int N, int K = 0>
+__device__ __forceinline__ void row_gj_nopiv(double (&w)[N], int r, double& myinv) {
+  if constexpr (K < N) {
+    const double inv = recip_newton(row_bcast_asm<K>(w[K]));
+    const double nf = r == K ? 0.0 : -(w[K] * inv);  // minus the multiple of row K in this row
+    if (r == K) myinv = inv;
+    elim_row<N, K>(w, nf);     // (column K: w[K] - p_K w[K] / p_K, replaced below)
+    w[K] = r == K ? 1.0 : nf;  // the inverse's column K (row K: p_K / p_K, scaled at the end)
+    row_gj_nopiv<N, K + 1>(w, r, myinv);
+  }
+}
+
 // Group maximum of a 32-bit unsigned key over the 16 lanes of a DPP row
 // (each step's DPP move fuses into v_max_u32).
 __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
@@ -953,13 +1027,6 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
   v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppHalfMirror, 0xf, 0xf, false));
   v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kDppMirror, 0xf, 0xf, false));
   return v;
-}
-
-// 1 / x to within an ulp or so (v_rcp_f64 and two Newton steps): x finite, nonzero
-__device__ __forceinline__ double recip_newton(double x) {
-  double y = __builtin_amdgcn_rcp(x);
-  y = fma(y, fma(-x, y, 1.0), y);
-  return fma(y, fma(-x, y, 1.0), y);
 }
 
 // group_gj_invert for the row kernel (one problem per 16-lane DPP row): the
@@ -1134,24 +1201,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     ++it;
     double wi[N];
     {
-      double w[N];
-      int col, pk[N];
+      double w[N], w0[N];
 #pragma unroll
       for (int j = 0; j < N; ++j) w[j] = j == r ? 1.0 : 0.0;
       bmul_acc<N>(gr, hr, w);  // W = I + G H
-      if (!row_gj_invert<N>(w, r, Tl, pk, &col)) {
-        st = QT_DARE_SINGULAR;
-        continue;
-      }
-      // W^-1[a][pk[k]] = S[pk[a]][k]: lane pk[a] (col = a) scatters its row to row a
-      if (col >= 0) {
 #pragma unroll
-        for (int k = 0; k < N; ++k) Tl[col * S + pk[k]] = w[k];
-      }
-      wave_sync();
+      for (int j = 0; j < N; ++j) w0[j] = w[j];
+      // W^-1 without row exchanges (row_gj_nopiv), checked by the residual of
+      // W (W^-1 1) = 1; a problem that misses it takes row_gj_invert's
+      double myinv = 1.0, srow = 0.0;
+      row_gj_nopiv<N>(w, r, myinv);
 #pragma unroll
-      for (int j = 0; j < N; ++j) wi[j] = Tl[rc * S + j];
-      wave_sync();
+      for (int j = 0; j < N; ++j) w[j] *= myinv, srow += w[j];
+      double res = -1.0;
+      dot_lanes<N>(res, srow, w0);
+      const bool gbad = !group_all<GS>(!(r < N) || fabs(res) <= kInvCheck);
+      if (__ballot(gbad) != 0) {
+        int col, pk[N];
+        double w2[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) w2[j] = w0[j];
+        const bool ok = row_gj_invert<N>(w2, r, Tl, pk, &col);
+        if (ok) {
+          // W^-1[a][pk[k]] = S[pk[a]][k]: lane pk[a] (col = a) scatters its row to row a
+          if (col >= 0) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) Tl[col * S + pk[k]] = w2[k];
+          }
+          wave_sync();
+#pragma unroll
+          for (int j = 0; j < N; ++j) w2[j] = Tl[rc * S + j];
+          wave_sync();
+        }
+        if (gbad) {
+          if (!ok) st = QT_DARE_SINGULAR;
+#pragma unroll
+          for (int j = 0; j < N; ++j) w[j] = w2[j];
+        }
+      }
+      if (st != QT_DARE_OK) continue;
+#pragma unroll
+      for (int j = 0; j < N; ++j) wi[j] = w[j];
     }
     // Y2 = Winv G ; Y1 = Winv A ; T2 = Y2 A' ; T = H Y1 ; A_next = A Y1
     double y1[N], y2[N], t[N], t2[N], an[N], u[N];

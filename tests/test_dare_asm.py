@@ -3,13 +3,15 @@ fmac_col) against gfx950's DPP hazards, on the device assembly built with the
 library's own flags (Makefile `dare-asm`; CPU only, hipcc cross-compiles).
 
 The compiler's hazard recognizer does not look inside inline asm, so the
-kernel states its rule and this test checks it on every v_fmac_f64_dpp:
+kernel states its rule and this test checks it on every DPP instruction of
+the row kernels (the asm FMAs and moves, and the compiler's own DPP, whose
+sources inline asm may have written):
   * no VALU instruction writing the DPP source (src0) VGPRs within the 2 wait
     states before it;
-  * no EXEC write (v_cmpx, or a scalar instruction with exec as destination)
-    within the 5 wait states before it;
-  * no label (a branch target, whose predecessors are not in view) inside that
-    5-wait-state window.
+  * no VALU write of EXEC (v_cmpx) within the 5 wait states before it (the
+    hazard LLVM's recognizer models; scalar EXEC writes are not one);
+  * along every path into the instruction (fall-through and branches to the
+    labels in that window).
 Each instruction is one wait state, `s_nop N` is N + 1."""
 
 import os
@@ -54,31 +56,52 @@ def _ops(text):
 
 
 def _hazards(lines):
-    """(line index, reason) of every v_fmac_f64_dpp that breaks the rule."""
-    bad = []
-    for i, text in enumerate(lines):
-        if not text.startswith("v_fmac_f64_dpp"):
-            continue
-        _, ops = _ops(text.split(" row_newbcast")[0])
-        src0 = _vregs(ops[1])
-        ws = 0
-        for j in range(i - 1, -1, -1):
+    """(line index, reason) of every DPP instruction that breaks the rule.
+    Walking back across a label follows every way into it: the fall-through
+    (unless an unconditional branch ends the block above) and every branch to
+    it."""
+    branches = {}
+    for j, t in enumerate(lines):
+        m = re.match(r"s_(?:c?branch\w*)\s+(\.LBB\S+)", t)
+        if m:
+            branches.setdefault(m.group(1) + ":", []).append(j)
+
+    def walk(j, ws, src0, seen):
+        """Hazard reason walking back from line j with ws wait states behind, or None."""
+        while j >= 0 and ws < 5:
             prev = lines[j]
-            if prev.endswith(":"):  # a label: a branch may enter here
-                bad.append((i, f"label {prev} within {ws} wait states"))
-                break
+            if prev.endswith(":"):  # a label: every way in
+                if (j, ws) in seen:
+                    return None
+                seen.add((j, ws))
+                for bj in branches.get(prev, []):
+                    why = walk(bj, ws, src0, seen)
+                    if why:
+                        return why
+                if j > 0 and lines[j - 1].startswith("s_branch"):
+                    return None
+                j -= 1
+                continue
             op, pops = _ops(prev)
-            if op.startswith("v_cmpx") or (op.startswith("s_") and pops and pops[0].startswith("exec")) or \
-                    op.endswith("saveexec_b64"):
-                bad.append((i, f"EXEC write `{prev}` {ws} wait states before"))
-                break
+            if op.startswith("v_cmpx") or (op.startswith("v_") and pops and pops[0].startswith("exec")):
+                return f"EXEC write `{prev}` {ws} wait states before"
             if op.startswith("v_") and not op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")) and pops:
                 if _vregs(pops[0]) & src0 and ws < 2:
-                    bad.append((i, f"VALU write of the DPP source `{prev}` {ws} wait states before"))
-                    break
+                    return f"VALU write of the DPP source `{prev}` {ws} wait states before"
             ws += int(pops[0]) + 1 if op == "s_nop" else 1
-            if ws >= 5:
-                break
+            j -= 1
+        if j < 0 and ws < 5:
+            return "kernel entry within the window"
+        return None
+
+    bad = []
+    for i, text in enumerate(lines):
+        if not re.match(r"v_\w+_dpp\b", text):
+            continue
+        _, ops = _ops(re.split(r" (?:row_|quad_perm)", text)[0])
+        why = walk(i - 1, 0, _vregs(ops[1]), set())
+        if why:
+            bad.append((i, why))
     return bad
 
 
@@ -107,7 +130,11 @@ def test_checker_catches_hazards():
     assert _hazards(ok) == []
     write = ["s_nop 4", "v_mov_b64_e32 v[2:3], v[8:9]", ok[1]]
     assert _hazards(write) and "VALU write" in _hazards(write)[0][1]
-    exe = ["s_and_saveexec_b64 s[4:5], vcc", "v_mov_b32_e32 v9, 0", ok[1]]
+    exe = ["v_cmpx_lt_f64_e32 vcc, 0, v[6:7]", "v_mov_b32_e32 v9, 0", ok[1]]
     assert _hazards(exe) and "EXEC" in _hazards(exe)[0][1]
-    lab = [".LBB0_3:", "v_mov_b32_e32 v9, 0", ok[1]]
-    assert _hazards(lab) and "label" in _hazards(lab)[0][1]
+    # a branch into the block from a point 1 wait state after writing the source
+    lab = ["s_nop 4", "v_mov_b64_e32 v[2:3], v[8:9]", "s_cbranch_vccz .LBB0_3", "s_nop 4", ".LBB0_3:", ok[1]]
+    assert _hazards(lab) and "VALU write" in _hazards(lab)[0][1]
+    # the same with a long fall-through path only: clean
+    assert _hazards(["s_nop 4", "v_mov_b64_e32 v[2:3], v[8:9]", "s_nop 4", ".LBB0_3:", "v_mov_b32_e32 v9, 0",
+                     ok[1]]) == []
