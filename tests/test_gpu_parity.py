@@ -665,6 +665,47 @@ def test_dense_dare_batch_edge_sizes(qt, n, p):
         solve_dare(np.eye(2), np.ones((2, 9)), np.eye(2), np.eye(9))
 
 
+@pytest.mark.parametrize("n", [2, 7])
+def test_dense_dare_row_exchange_fallback(qt, n):
+    """A problem whose first doubling matrix W = I + G Q has W[0][0] = 0
+    exactly (G = b b' with b = [1, 2, 0..], Q = c c' + diag(0, 0, 1..) with
+    c = [1, -1, 0..]): the row kernel's inverse without row exchanges breaks
+    down there, its residual check sends the problem to the pivoted
+    inversion, and the result is the DARE's solution.  It shares its
+    wavefront with benign problems, which keep the exchange-free path; every
+    problem satisfies its DARE and K = (R + B'PB)^-1 B'PA.  n = 2 and 7 reach
+    the 6- and 9-row kernels."""
+    from quadtrack import core
+
+    rng = np.random.default_rng(11)
+    m, p = 8, 1
+    b0 = np.zeros((n, p))
+    b0[:2, 0] = [1.0, 2.0]
+    c0 = np.zeros(n)
+    c0[:2] = [1.0, -1.0]
+    q0 = np.outer(c0, c0) + np.diag([0.0, 0.0] + [1.0] * (n - 2))
+    A = np.stack([0.5 * np.eye(n) + (0 if i % 2 == 0 else 0.1 * rng.normal(size=(n, n))) for i in range(m)])
+    B = np.stack([b0 if i % 2 == 0 else rng.normal(size=(n, p)) for i in range(m)])
+    Q = np.stack([q0 if i % 2 == 0 else np.eye(n) for i in range(m)])
+    R = np.stack([np.eye(p) for _ in range(m)])
+    assert (np.eye(n) + B[0] @ B[0].T @ Q[0])[0, 0] == 0.0
+    dev = torch.device("cuda:0")
+
+    def soa(x):
+        return torch.as_tensor(np.ascontiguousarray(x.reshape(m, -1).T), device=dev)
+
+    K, P, st, it = core.dare_dense(soa(A), soa(B), soa(Q), soa(R), ab_per_problem=True)
+    assert st.cpu().tolist() == [0] * m
+    K = K.cpu().numpy().T.reshape(m, p, n)
+    P = P.cpu().numpy().T.reshape(m, n, n)
+    for i in range(m):
+        a, b, q, r, pp = A[i], B[i], Q[i], R[i], P[i]
+        btp = b.T @ pp
+        res = a.T @ pp @ a - pp - a.T @ pp @ b @ np.linalg.solve(r + btp @ b, btp @ a) + q
+        assert np.max(np.abs(res)) <= 1e-9 * max(1.0, np.max(np.abs(pp))), (i, np.max(np.abs(res)))
+        np.testing.assert_allclose(K[i], np.linalg.solve(r + btp @ b, btp @ a), rtol=1e-8, atol=1e-11)
+
+
 # ------------------------------------------------------- component kernels
 
 
