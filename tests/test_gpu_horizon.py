@@ -3,7 +3,7 @@
 the same episodes, for 12 seeded configurations that push each stop
 condition into the horizons — low speed clamps, close position bounds, odd
 episode lengths, other time steps and rate limits, light and heavy plants,
-LQR / LQI / PID.  Decisions (steps, termination codes, counts) must be
+LQR / LQI / PID, the last three with the Euler integrator.  Decisions (steps, termination codes, counts) must be
 identical, values within 1e-9 (the two paths contract FMAs differently).
 Both are also checked against the oracle (oracle/qt_oracle.c, the reference's
 step restated) run on the same limits, masses, seeds and controller: step
@@ -37,6 +37,8 @@ def _config(i):
                           "max_position": float(r.uniform(3.0, 30.0)),
                           "max_episode_time": float(np.round(r.uniform(4.0, 12.0), 3))},
            "quadcopter": {"max_angular_rate": 3.0}}
+    if i >= 12:  # the Euler closed form (make_rate_lin) under the same randomised limits
+        env["simulation"]["integrator"] = "euler"
     kind = ["riccati_lqr", "lqi", "pid"][i % 3]
     ctl = {"dt": dt, "max_rate": float(r.uniform(1.0, 3.0))}
     if kind == "riccati_lqr":
@@ -45,7 +47,7 @@ def _config(i):
     return env, kind, ctl, mass
 
 
-@pytest.mark.parametrize("i", range(12))
+@pytest.mark.parametrize("i", range(15))
 def test_horizon_randomised_limits(qt, i):
     from quadtrack.controllers import batched_controller
     from quadtrack.rollout import run_closed_loop
