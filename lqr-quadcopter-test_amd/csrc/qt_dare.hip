@@ -40,6 +40,29 @@ __device__ __forceinline__ void heuristic_axis(double qp, double qv, double r, d
   kv = sqrt(2.0 * sqrt(qp / r) + qv / r);
 }
 
+// A failed problem's gain row r (r < p): zeros, or with `heuristic` the
+// fallback gains (riccati_lqr.py:756-774, controllers/__init__.py:537-572) —
+// row 0 (thrust) from the z axis, row 1 (roll) from -y, row 2 (pitch) from x.
+// Each lane writes its own row, whole: one writer per K entry.
+template <int N>
+__device__ __forceinline__ void store_failed_gain_row(int r, int n, int p, int64_t m, int64_t pb, const double* q,
+                                                      const double* rin, bool heuristic, double* K) {
+  int c0 = -1;
+  double kp = 0.0, kv = 0.0;
+  if (heuristic && r < 3) {
+    auto qd = [&](int i) { return q[(int64_t)(i * n + i) * m + pb]; };
+    auto rd = [&](int i) { return rin[(int64_t)(i * p + i) * m + pb]; };
+    const double rrate = (rd(1) + rd(2) + rd(3)) / 3.0;
+    const int ax = 2 - r;
+    heuristic_axis(qd(ax), qd(3 + ax), r == 0 ? rd(0) : rrate, kp, kv);
+    if (r == 1) kp = -kp, kv = -kv;
+    c0 = ax;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (j < n) K[(int64_t)(r * n + j) * m + pb] = j == c0 ? kp : (c0 >= 0 && j == c0 + 3 ? kv : 0.0);
+}
+
 // ------------------------------------------------------------ axis kernel
 
 // N = 2 (LQR axis: pos, vel) or 3 (LQI axis: pos, vel, integral).
@@ -802,35 +825,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVE
         if (j < n) P[(int64_t)(r * n + j) * m + pb] = Hl[r * S + j];
     }
   } else {
-    if (r < p) {
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (j < n) K[(int64_t)(r * n + j) * m + pb] = 0.0;
-    }
+    if (r < p) store_failed_gain_row<N>(r, n, p, m, pb, q, rin, fallback && hover, K);
     if (P && r < n) {
 #pragma unroll
       for (int j = 0; j < N; ++j)
         if (j < n) P[(int64_t)(r * n + j) * m + pb] = 0.0;
     }
   }
-  // one status / fallback per problem (st is uniform over the group), from its first lane
+  // one status per problem (st is uniform over the group), from its first lane
   if (r == 0) {
-    if (!ok && fallback && hover) {
-      // heuristic gains from the diagonals (riccati_lqr.py:756-774)
-      auto qd = [&](int i) { return q[(int64_t)(i * n + i) * m + pb]; };
-      auto rd = [&](int i) { return rin[(int64_t)(i * p + i) * m + pb]; };
-      const double rrate = (rd(1) + rd(2) + rd(3)) / 3.0;
-      double kp, kv;
-      heuristic_axis(qd(2), qd(5), rd(0), kp, kv);
-      K[(int64_t)(0 * n + 2) * m + pb] = kp;
-      K[(int64_t)(0 * n + 5) * m + pb] = kv;
-      heuristic_axis(qd(1), qd(4), rrate, kp, kv);
-      K[(int64_t)(1 * n + 1) * m + pb] = -kp;
-      K[(int64_t)(1 * n + 4) * m + pb] = -kv;
-      heuristic_axis(qd(0), qd(3), rrate, kp, kv);
-      K[(int64_t)(2 * n + 0) * m + pb] = kp;
-      K[(int64_t)(2 * n + 3) * m + pb] = kv;
-    }
     status[pb] = (int8_t)st;
     if (iters) iters[pb] = it;
   }
@@ -1087,6 +1090,12 @@ __device__ __forceinline__ void lds_transpose(double* buf, const double (&row)[N
 #define QT_DARE_SYM 1
 #endif
 
+// the pivoted inversion behind the row kernel's residual check (0 only for
+// instruction counts of the common path)
+#ifndef QT_DARE_FALLBACK
+#define QT_DARE_FALLBACK 1
+#endif
+
 #ifndef QT_DARE_ROW_WAVES
 #define QT_DARE_ROW_WAVES 2  // minimum waves per SIMD the row kernel's register allocation must allow
 #endif
@@ -1216,7 +1225,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
       double res = -1.0;
       dot_lanes<N>(res, srow, w0);
       const bool gbad = !group_all<GS>(!(r < N) || fabs(res) <= kInvCheck);
-      if (__ballot(gbad) != 0) {
+      if (QT_DARE_FALLBACK && __ballot(gbad) != 0) {
         int col, pk[N];
         double w2[N];
 #pragma unroll
@@ -1335,25 +1344,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     for (int j = 0; j < N; ++j)
       if (j < n) P[(int64_t)(r * n + j) * m + pb] = ok ? Hl[r * S + j] : 0.0;
   }
-  if (!ok && r < p) {
-    // a failed problem: zero gains, or the heuristic ones (riccati_lqr.py:756-774,
-    // controllers/__init__.py:537-572), each row written by its own lane:
-    // row 0 (thrust) from the z axis, row 1 (roll) from -y, row 2 (pitch) from x
-    int c0 = -1;
-    double kp = 0.0, kv = 0.0;
-    if (fallback && hover && r < 3) {
-      auto qd = [&](int i) { return q[(int64_t)(i * n + i) * m + pb]; };
-      auto rd = [&](int i) { return rin[(int64_t)(i * p + i) * m + pb]; };
-      const double rrate = (rd(1) + rd(2) + rd(3)) / 3.0;
-      const int ax = 2 - r;
-      heuristic_axis(qd(ax), qd(3 + ax), r == 0 ? rd(0) : rrate, kp, kv);
-      if (r == 1) kp = -kp, kv = -kv;
-      c0 = ax;
-    }
-#pragma unroll
-    for (int j = 0; j < N; ++j)
-      if (j < n) K[(int64_t)(r * n + j) * m + pb] = j == c0 ? kp : (c0 >= 0 && j == c0 + 3 ? kv : 0.0);
-  }
+  if (!ok && r < p) store_failed_gain_row<N>(r, n, p, m, pb, q, rin, fallback && hover, K);
   if (r == 0) {
     status[pb] = (int8_t)st;
     if (iters) iters[pb] = it;
