@@ -1087,7 +1087,7 @@ __device__ __forceinline__ void lds_transpose(double* buf, const double (&row)[N
 // does; 0: add M as computed (A' (H W^-1) A and A (W^-1 G) A' are symmetric in
 // exact arithmetic: H W^-1 = (I + H G)^-1 H), which spares two LDS transposes
 #ifndef QT_DARE_SYM
-#define QT_DARE_SYM 1
+#define QT_DARE_SYM 0
 #endif
 
 // the pivoted inversion behind the row kernel's residual check (0 only for
