@@ -316,8 +316,9 @@ def main():
         # the dominant kernel: the fast yaw-at-rest flavour (older profiles: the single-flavour kernel)
         traffic, traffic_src = pmc_traffic(args.profile_dir, KERNEL_TAG)
         # algorithmic HBM bytes of one fresh launch: per-episode pattern 3 and start offset 3 doubles
-        # in; x 12, target 9, t, acc 14 and the 14 metric rows out; gains are a broadcast
-        algo_bytes = (6 + 50) * 8 * n
+        # in; x 12, target 9, t, acc 14, the 14 metric rows and the 3 integral rows qt_reset would
+        # zero out; gains are a broadcast
+        algo_bytes = (6 + 53) * 8 * n
         # the same frac from the committed rocprofv3 kernel trace (fast launch alone; its deferred
         # exact pass runs no wave at this workload)
         prof = profiled_kernel(args.profile_dir, KERNEL_TAG)
