@@ -602,7 +602,15 @@ __device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizo
 // length k that began on->off, <= 0 off target outside a phase; a phase's
 // running maximum `cur` restarts at the on-target step's err - R <= 0, which
 // any off-target excess > 0 replaces.
-template <int MOTION, int KC, bool FF, bool KS, bool UNI>
+// DUAL: a second no-vote body that applies the tilt clamp, for waves whose
+// tilt-bounded horizon is short because some lane sits at (or near) the tilt
+// clamp (config 4's tuner candidates: 46% of a wave's steps were voted).  Such
+// a wave bounds its horizon without the tilt (speed, position, time only) and
+// runs it with the clamp in every step — exactly the voted step without the
+// vote, so results are bitwise those of the voted loop.
+constexpr int kDualBelow = 8;  // tilt-bounded horizons shorter than this try the clamping body
+
+template <int MOTION, int KC, bool FF, bool KS, bool UNI, bool DUAL = false>
 __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                          int motion, const Pattern& pt, const Plant& pl_lane, double hover,
                                          const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
@@ -661,8 +669,8 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
     int rem = nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0;  // steps left in this run (z stays < 1 off phase)
     RateCoef rk;
     // one closed-loop step; VOTE: end it with the stop vote (true: stop here)
-    auto step = [&](auto vote, const double* fc, const double* fs) -> bool {
-      constexpr bool VOTE = decltype(vote)::value;
+    auto step = [&](auto vote, auto clamp, const double* fc, const double* fs) -> bool {
+      constexpr bool VOTE = decltype(vote)::value, CLAMP = decltype(clamp)::value;
       rk.pin();
       const double a0[2] = {x[6], x[7]};  // step-start roll / pitch (attitude_trig_resid)
       // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -719,7 +727,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       // in every voted step and (!kTiltHorizon) in the horizon's steps too
       if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain_fast_apply<true>(e, x);
       attitude_trig_resid(x + 6, a0, d4, t4, ta);
-      if ((VOTE || !kTiltHorizon) && !(QT_ABLATE & QT_ABL_CONSTRAIN)) tilt_clamp(x, ta);
+      if ((VOTE || CLAMP || !kTiltHorizon) && !(QT_ABLATE & QT_ABL_CONSTRAIN)) tilt_clamp(x, ta);
       // the stop conditions as one maximum >= 0 (the state is finite): speed
       // at the clamp's guard band, position bounds, time limit, end of the run
       // (rem, uniform) — one compare and one
@@ -735,31 +743,51 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
     // The safe horizon's steps without the vote (four per back edge, then
     // the horizon's last two); voted steps only where no horizon is left.
     do {
-      const int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
+      int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
+      bool clamp_body = false;  // wave-uniform (H comes from ballots)
+      if constexpr (DUAL) {
+        if (H < kDualBelow) {
+          const int H2 = yaw0_horizon<false, kFold>(e, k.hz, lin, pl, x, t, rem);
+          if (H2 > H) H = H2, clamp_body = true;
+        }
+      }
+      using F = std::false_type;
+      using T = std::true_type;
       if constexpr (kFold) {
         double fc[3], fs[3];  // the horizon's folded target rotor
         rotor_fold<MOTION>(k, ((t + e.dt) - t) - e.dt, fc, fs);
         for (int j = 4; j <= H; j += 4) {
-          step(std::false_type{}, fc, fs);
-          step(std::false_type{}, fc, fs);
-          step(std::false_type{}, fc, fs);
-          step(std::false_type{}, fc, fs);
+          step(F{}, F{}, fc, fs);
+          step(F{}, F{}, fc, fs);
+          step(F{}, F{}, fc, fs);
+          step(F{}, F{}, fc, fs);
         }
         if (H & 2) {
-          step(std::false_type{}, fc, fs);
-          step(std::false_type{}, fc, fs);
+          step(F{}, F{}, fc, fs);
+          step(F{}, F{}, fc, fs);
+        }
+      } else if (DUAL && clamp_body) {
+        for (int j = 4; j <= H; j += 4) {
+          step(F{}, T{}, nullptr, nullptr);
+          step(F{}, T{}, nullptr, nullptr);
+          step(F{}, T{}, nullptr, nullptr);
+          step(F{}, T{}, nullptr, nullptr);
+        }
+        if (H & 2) {
+          step(F{}, T{}, nullptr, nullptr);
+          step(F{}, T{}, nullptr, nullptr);
         }
       } else {
         // four steps per back edge, then the horizon's last two (H is even)
         for (int j = 4; j <= H; j += 4) {
-          step(std::false_type{}, nullptr, nullptr);
-          step(std::false_type{}, nullptr, nullptr);
-          step(std::false_type{}, nullptr, nullptr);
-          step(std::false_type{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
         }
         if (H & 2) {
-          step(std::false_type{}, nullptr, nullptr);
-          step(std::false_type{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
+          step(F{}, F{}, nullptr, nullptr);
         }
       }
       rem -= H;
@@ -770,7 +798,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       // every step is voted.
       const int nv = H > 0 ? 0 : (k.hz.on ? kVotedBurst : (1 << 30));
       bool stop = false;
-      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{}, nullptr, nullptr);
+      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{}, std::false_type{}, nullptr, nullptr);
       if (stop) break;
     } while (true);
     const int ran = (nsteps - s0 > (1 << 29) ? (1 << 29) : nsteps - s0) - rem;
@@ -908,7 +936,10 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     if constexpr (FLAVOR == kYaw0)
-      run_yaw0<MOTION, KC, FF, KS, UNI>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, lc);
+      run_yaw0<MOTION, KC, FF, KS, UNI,
+               FRESH && KC != 9 && (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
+                                    MOTION == QT_MOTION_FIGURE8)>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ,
+                                                                  tg, t, a, nsteps, lc);
     else
       run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec,
                                           n, ep);

@@ -46,9 +46,17 @@ def step_loops(blocks):
     next block of > 100 instructions whose branch tests the vote, vcc)."""
     out = []
     big = [b for b in blocks if b["n"] > 100]
+
+    def no_vote(b):
+        return any(br.endswith(" " + b["name"]) for br in b["br"]) and not any("vcc" in br for br in b["br"])
+
     for i, b in enumerate(big):
-        if any(br.endswith(" " + b["name"]) for br in b["br"]) and not any("vcc" in br for br in b["br"]):
-            voted = next((v for v in big[i + 1:] if any("vcc" in br for br in v["br"])), None)
+        if no_vote(b):
+            # the voted step: the next big block that ends in the vote (skipping a
+            # second no-vote body, run_yaw0's DUAL clamping one)
+            is_voted = lambda v: any("vcc" in br for br in v["br"]) and not no_vote(v)  # noqa: E731
+            voted = next((v for v in big[i + 1:] if is_voted(v)), None) or \
+                next((v for v in reversed(big[:i]) if is_voted(v)), None)
             out.append((b, voted))
     return out
 
