@@ -15,8 +15,9 @@
 //    single-input axes (x <- pitch rate, y <- roll rate, z <- thrust) and a
 //    yaw row that is identically zero.  One lane per (problem, axis): the
 //    2x2 / 3x3 axis DARE lives entirely in registers.
-//  * dare_dense_kernel — arbitrary symmetric Q (6x6 / 9x9) and R (4x4): one
-//    wavefront per problem, matrices in LDS, cooperative LU + products.
+//  * dare_row_kernel — arbitrary symmetric Q and R and general A, B (n <= 16,
+//    p <= 8): one problem per 16-lane DPP row, row r of every matrix in lane
+//    r's registers, products by DPP-broadcast FMAs (below).
 // Both validate Q (PSD) and R (PD) like _is_positive_semidefinite /
 // _is_positive_definite (riccati_lqr.py:57-116) and fall back to the
 // heuristic gains of LQRController._compute_gains (controllers/__init__.py:
@@ -303,26 +304,22 @@ constexpr int kMaxN = 16, kMaxP = 8;
 #ifndef QT_DARE_ROWS_IN_FLIGHT
 #define QT_DARE_ROWS_IN_FLIGHT 3  // rows of a product's right factor loaded ahead of their use
 #endif
-#ifndef QT_DARE_WAVES
-#define QT_DARE_WAVES 2  // minimum waves per SIMD the register allocation must allow
-#endif
 
-// ----------------------------------------------------------- dense kernel
+// ------------------------------------------------- dense-kernel helpers
 //
-// General dense SDA for n <= 16 states, p <= 8 inputs: a group of GS lanes
-// per problem (GS = 8 for n <= 6, else 16; one DPP row or half row), 64 / GS
-// problems per wavefront, lane r holding row r of every n x n matrix in
-// registers.  A product X Y reads X from the lane's own row and Y's rows from
-// LDS (the group's lanes read the same addresses: broadcasts); the
-// Gauss-Jordan solves broadcast the pivot row through LDS; reductions
-// (pivot search, norms) are DPP butterflies inside the group.  Every group
-// lives in one wavefront, so its LDS hand-offs need only wave-level ordering
-// (wave_sync): no workgroup barrier, no single-lane serial sections.
-// Sizes are compile-time (N, PP): 6 / 4 (hover LQR), 9 / 4 (hover LQI) and
-// 16 / 8 (anything else), the runtime n x n / p x p problem zero-padded to
-// them — padded rows and columns of A, B, Q, G, H are zero and R's padding is
-// the identity, which decouples them exactly (every padded term is an exact
-// +0 in each sum, pivots stay inside the real block).
+// Group-level pieces of the dense SDA (dare_row_kernel): a group of GS lanes
+// holds one problem, lane r row r of every n x n matrix; a product X Y reads
+// X from the lane's own row and (row_times) Y's rows from LDS, the group's
+// lanes reading the same addresses: broadcasts; Gauss-Jordan solves
+// broadcast the pivot row through LDS; reductions (pivot search, norms) are
+// DPP butterflies inside the group.  Every group lives in one wavefront, so
+// its LDS hand-offs need only wave-level ordering (wave_sync): no workgroup
+// barrier, no single-lane serial sections.  Sizes are compile-time (N, PP):
+// 6 / 4 (hover LQR), 9 / 4 (hover LQI) and 16 / 8 (anything else), the
+// runtime n x n / p x p problem zero-padded to them — padded rows and columns
+// of A, B, Q, G, H are zero and R's padding is the identity, which decouples
+// them exactly (every padded term is an exact +0 in each sum, pivots stay
+// inside the real block).
 
 // Wave-level ordering of LDS accesses: a wavefront's LDS operations complete
 // in issue order, so a compiler barrier is all a hand-off inside one
@@ -462,50 +459,6 @@ __device__ __forceinline__ bool group_gauss_jordan(double (&w)[NC], int r, doubl
   return true;
 }
 
-// In-place Gauss-Jordan inversion with partial pivoting of the group's
-// NR x NR matrix W, row r in this lane's w (lanes r >= NR hold no row).  Rows
-// are not swapped: pk[k] records the lane whose row became pivot k (the same
-// in every lane of the group) and *col the pivot this lane's row became.
-// Each step broadcasts the NR-entry pivot row through `piv` (LDS).  On return
-// the lanes hold S with  W^-1[a][pk[k]] = S[pk[a]][k],  so row a of W^-1 X is
-// sum_k S[pk[a]][k] X[pk[k]][:], which lane pk[a] (*col = a) forms by reading
-// X's rows in pk order.  Ties take the lowest row.  Returns false (uniform over
-// the group) when a pivot column is all zero.
-template <int NR, int GS>
-__device__ __forceinline__ bool group_gj_invert(double (&w)[NR], int r, double* piv, int (&pk)[NR], int* col) {
-  bool used = r >= NR;
-  *col = -1;
-#pragma unroll
-  for (int k = 0; k < NR; ++k) {
-    const double cand = used ? -1.0 : fabs(w[k]);
-    const double mx = group_max<GS>(cand);
-    if (!(mx > 0.0)) return false;
-    const int p = __builtin_ctz(group_bits<GS>(__ballot(!used && cand == mx)));
-    pk[k] = p;
-    if (r == p) {
-      const double inv = 1.0 / w[k];
-#pragma unroll
-      for (int j = 0; j < NR; ++j) w[j] = j == k ? inv : w[j] * inv;
-      st_row<NR, NR + (NR & 1)>(piv, 0, w);
-      used = true;
-      *col = k;
-    }
-    wave_sync();
-    if (r != p) {  // lanes r >= NR eliminate too: their values are never used
-      const double f = w[k];
-#pragma unroll
-      for (int j = 0; j + 1 < NR; j += 2) {
-        const double2 v = *reinterpret_cast<const double2*>(piv + j);
-        w[j] = j == k ? -f * v.x : w[j] - f * v.x;
-        w[j + 1] = j + 1 == k ? -f * v.y : w[j + 1] - f * v.y;
-      }
-      if (NR & 1) w[NR - 1] = NR - 1 == k ? -f * piv[NR - 1] : w[NR - 1] - f * piv[NR - 1];
-    }
-    wave_sync();
-  }
-  return true;
-}
-
 // Row-per-lane Cholesky test of the group's N x N matrix c (row r in this
 // lane): true iff every pivot is > 0, i.e. c is positive definite.  The
 // column of each step goes through `colbuf` (LDS, N doubles).
@@ -545,300 +498,6 @@ __device__ __forceinline__ bool group_symmetric(const double (&row)[N], int r, d
   return group_all<GS>(ok);
 }
 
-template <int N, int PP, int GS>
-struct GroupDims {
-  static constexpr int kProblemsPerWave = 64 / GS;
-  static constexpr int S = (N + 1) & ~1;                   // LDS row stride (doubles)
-  static constexpr int MAT = N * S;
-  static constexpr int RAW = 5 * MAT;                       // H, A, Y1, T (also the pivot / column buffer), G
-  // per-problem stride = 8 (mod 32) doubles: the 64 / GS problems of a wave
-  // start 16 banks apart, so their broadcast reads do not conflict
-  static constexpr int PROB = RAW + ((8 - RAW % 32) + 32) % 32;
-  static_assert(3 * N <= MAT && PP + N <= MAT && N <= GS && PP <= GS, "group layout");
-};
-
-
-template <int N, int PP, int GS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVES, 8))) void dare_group_kernel(int n, int p, int64_t m, const double* __restrict__ Ain,
-                                                        const double* __restrict__ Bin, int ab_per_problem,
-                                                        double dt, double gravity, const double* __restrict__ mass,
-                                                        const double* __restrict__ q, const double* __restrict__ rin,
-                                                        int fallback, double* K, double* P, int8_t* status,
-                                                        int32_t* iters) {
-  using D = GroupDims<N, PP, GS>;
-  constexpr int S = D::S, MAT = D::MAT, NC = 3 * N;
-  __shared__ __attribute__((aligned(16))) double lds[D::kProblemsPerWave * D::PROB];
-  const int lane = threadIdx.x & 63, g = lane / GS, r = lane % GS;
-  // rows read by lanes past the matrix (r >= N, r >= PP): a real row, so the
-  // loads need no branch; such lanes' values are never stored, never pivot
-  // and are zeroed before every group reduction
-  const int rc = r < N ? r : N - 1, rp = r < PP ? r : PP - 1;
-  const int64_t pb = (int64_t)blockIdx.x * D::kProblemsPerWave + g;
-  const bool valid = pb < m;  // uniform over the group
-  double* Hl = lds + g * D::PROB;
-  double* Al = Hl + MAT;
-  double* Yl = Al + MAT;
-  double* Tl = Yl + MAT;
-  double* Gl = Tl + MAT;
-  const bool hover = Ain == nullptr;
-  const double mss = (valid && mass) ? mass[pb] : 1.0;
-  const int64_t abm = ab_per_problem ? m : 1, abj = ab_per_problem ? pb : 0;
-  const bool real = valid && r < n;
-
-  // ---- inputs, read where they are used (the doubling loop keeps only G in
-  // registers across its solve): A, B (N-row padded), R (PP-row padded)
-  auto a_in = [&](int j) -> double {
-    if (!(real && j < n)) return 0.0;
-    if (!hover) return Ain[(int64_t)(r * n + j) * abm + abj];
-    double a = (r == j) ? 1.0 : 0.0;
-    if (r < 3 && j == r + 3) a = dt;             // A_d = I + A_c dt (riccati_lqr.py:260)
-    if (n == 9 && r >= 6 && j == r - 6) a = dt;  // integral rows (308)
-    return a;
-  };
-  auto b_in = [&](int c) -> double {
-    if (!(real && c < p)) return 0.0;
-    if (!hover) return Bin[(int64_t)(r * p + c) * abm + abj];
-    if (r == 5 && c == 0) return 1.0 / mss * dt;  // riccati_lqr.py:250,261
-    if (r == 4 && c == 1) return -gravity * dt;   // 252
-    if (r == 3 && c == 2) return gravity * dt;    // 254
-    return 0.0;
-  };
-  auto r_in = [&](int c) -> double {
-    return (valid && r < p && c < p) ? rin[(int64_t)(r * p + c) * m + pb] : (r == c ? 1.0 : 0.0);
-  };
-
-  // ---- validation (_is_positive_semidefinite / _is_positive_definite,
-  // riccati_lqr.py:57-116): symmetric within np.allclose, then the
-  // eigenvalue bounds as Cholesky tests: min eig(Q) >= -1e-10 <=> Q + 1e-10 I
-  // positive definite, min eig(R) > 1e-10 <=> R - 1e-10 I positive definite
-  // (the same decisions but on the boundary itself, to rounding)
-  double Hr[N];  // H = Q to start
-#pragma unroll
-  for (int j = 0; j < N; ++j) Hr[j] = (real && j < n) ? q[(int64_t)(r * n + j) * m + pb] : 0.0;
-  int st = QT_DARE_OK;
-  {
-    bool qok = group_symmetric<N, S, GS>(Hr, r, Tl);
-    double c[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) c[j] = Hr[j] + ((r == j) ? 1e-10 : 0.0);
-    qok = group_cholesky_pd<N, GS>(c, r, Tl) && qok;
-    double rr[PP];
-#pragma unroll
-    for (int j = 0; j < PP; ++j) rr[j] = r_in(j);
-    bool rok = group_symmetric<PP, S, GS>(rr, r, Tl);
-#pragma unroll
-    for (int j = 0; j < PP; ++j) rr[j] -= (r == j) ? 1e-10 : 0.0;
-    rok = group_cholesky_pd<PP, GS>(rr, r, Tl) && rok;
-    st = !qok ? QT_DARE_Q_NOT_PSD : (!rok ? QT_DARE_R_NOT_PD : QT_DARE_OK);
-  }
-
-  // ---- G = B R^-1 B': X = R^-1 B' by Gauss-Jordan on [R | B'] (lanes r < PP), G = B X
-  double Gr[N];
-  int it = 0;
-  bool conv = false;
-  {
-    double br[PP];
-#pragma unroll
-    for (int c = 0; c < PP; ++c) br[c] = b_in(c);
-    if (r < N) st_row<PP, S>(Yl, r, br);  // B (N x PP) for its columns
-    wave_sync();
-    double w[PP + N];
-#pragma unroll
-    for (int c = 0; c < PP; ++c) w[c] = r_in(c);
-#pragma unroll
-    for (int j = 0; j < N; ++j) w[PP + j] = r < PP ? Yl[j * S + rp] : 0.0;
-    wave_sync();
-    int col;
-    const bool ok = group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col);
-    if (st == QT_DARE_OK && !ok) st = QT_DARE_SINGULAR;
-    if (col >= 0) st_row<N, S>(Yl, col, w + PP);  // X row `col`
-    wave_sync();
-    row_times<PP, N, S>(br, Yl, Gr);
-    wave_sync();
-  }
-  if (r < N) {
-    double ar[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) ar[j] = a_in(j);
-    st_row<N, S>(Hl, r, Hr);
-    st_row<N, S>(Al, r, ar);
-  }
-  wave_sync();
-
-  // ---- doublings (the SDA iteration of dare_axis_kernel / riccati_lqr.py's
-  // fixed point): W = I + G H ; [Y1 Y2] = W^-1 [A G] ; H += sym(A' H Y1) ;
-  // G += sym(A Y2 A') ; A = A Y1, until |dH|_F <= tol |H|_F.  H, A and G's
-  // copy live in LDS (Hl, Al, Gl); W^-1 comes from an in-place inversion
-  // (N-entry pivot rows) and is applied to A and G as products; every
-  // intermediate product goes back to LDS at once (short register lifetimes).
-  if (r < N) st_row<N, S>(Gl, r, Gr);
-  wave_sync();
-  while (true) {
-    const bool act = valid && st == QT_DARE_OK && !conv && it < kMaxIter;  // uniform over the group
-    if (__ballot(act) == 0) break;
-    if (!act) continue;
-    ++it;
-    int col, pk[N];
-    {
-      double w[N];
-      row_times<N, N, S>(Gr, Hl, w);  // W = G H, then + I
-#pragma unroll
-      for (int j = 0; j < N; ++j) w[j] = j == r ? w[j] + 1.0 : w[j];
-      if (!group_gj_invert<N, GS>(w, r, Tl, pk, &col)) {
-        st = QT_DARE_SINGULAR;
-        continue;
-      }
-      // Y1, Y2 rows `col`: sum_k S[k] A[pk[k]], sum_k S[k] G[pk[k]]
-      double y1[N], y2[N];
-#pragma unroll
-      for (int j = 0; j < N; ++j) y1[j] = 0.0, y2[j] = 0.0;
-#pragma unroll
-      for (int k = 0; k < N; ++k) {
-        const double* ar = Al + pk[k] * S;
-        const double* gp = Gl + pk[k] * S;
-#pragma unroll
-        for (int j = 0; j + 1 < N; j += 2) {
-          const double2 a = *reinterpret_cast<const double2*>(ar + j);
-          const double2 gg = *reinterpret_cast<const double2*>(gp + j);
-          y1[j] += w[k] * a.x, y1[j + 1] += w[k] * a.y;
-          y2[j] += w[k] * gg.x, y2[j + 1] += w[k] * gg.y;
-        }
-        if (N & 1) y1[N - 1] += w[k] * ar[N - 1], y2[N - 1] += w[k] * gp[N - 1];
-      }
-      if (col >= 0) {
-        st_row<N, S>(Yl, col, y1);
-        st_row<N, S>(Tl, col, y2);
-      }
-    }
-    wave_sync();
-    double y2[N], t[N], hr[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) y2[j] = Tl[rc * S + j], hr[j] = Hl[rc * S + j];
-    // T = H Y1 ; M = A' T ; H' = H + (M + M') / 2
-    row_times<N, N, S>(hr, Yl, t);
-    wave_sync();
-    if (r < N) st_row<N, S>(Tl, r, t);
-    wave_sync();
-    {
-      double ac[N];  // column r of A
-#pragma unroll
-      for (int l = 0; l < N; ++l) ac[l] = Al[l * S + rc];
-      row_times<N, N, S>(ac, Tl, t);
-    }
-    wave_sync();
-    if (r < N) st_row<N, S>(Tl, r, t);
-    wave_sync();
-    double dn = 0.0, hn = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const double hnew = hr[j] + 0.5 * (t[j] + Tl[j * S + rc]);
-      dn += (hnew - hr[j]) * (hnew - hr[j]);
-      hn += hnew * hnew;
-      hr[j] = hnew;
-    }
-    dn = group_sum<GS>(r < N ? dn : 0.0);
-    hn = group_sum<GS>(r < N ? hn : 0.0);
-    const int flag = !isfinite(hn) ? -1 : (sqrt(dn) <= kTol * sqrt(hn) ? 1 : 0);
-    wave_sync();
-    if (r < N) st_row<N, S>(Hl, r, hr);
-    // T = Y2 A' ; M = A T ; G' = G + (M + M') / 2
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      double s2 = 0.0;
-#pragma unroll
-      for (int l = 0; l + 1 < N; l += 2) {
-        const double2 a = ld2<S>(Al, j, l);
-        s2 += y2[l] * a.x;
-        s2 += y2[l + 1] * a.y;
-      }
-      if (N & 1) s2 += y2[N - 1] * Al[j * S + N - 1];
-      t[j] = s2;
-    }
-    wave_sync();
-    if (r < N) st_row<N, S>(Tl, r, t);
-    wave_sync();
-    double ar[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) ar[j] = Al[rc * S + j];
-    row_times<N, N, S>(ar, Tl, t);
-    wave_sync();
-    if (r < N) st_row<N, S>(Tl, r, t);
-    wave_sync();
-#pragma unroll
-    for (int j = 0; j < N; ++j) Gr[j] += 0.5 * (t[j] + Tl[j * S + rc]);
-    // A = A Y1
-    row_times<N, N, S>(ar, Yl, t);
-    wave_sync();
-    if (r < N) {
-      st_row<N, S>(Al, r, t);
-      st_row<N, S>(Gl, r, Gr);
-    }
-    wave_sync();
-    if (flag < 0) st = QT_DARE_NO_CONVERGE;
-    if (flag == 1) conv = true;
-  }
-  if (valid && st == QT_DARE_OK && !conv) st = QT_DARE_NO_CONVERGE;
-
-  // ---- K = (R + B'PB)^-1 B'PA (riccati_lqr.py:181-182): T = B'P (lanes r < PP),
-  // W = R + T B, Y = T A0, solve W K = Y
-  if (valid && st == QT_DARE_OK) {
-    // B (for its columns and rows) and the original A back to LDS
-    wave_sync();
-    if (r < N) {
-      double br[PP], ar[N];
-#pragma unroll
-      for (int c = 0; c < PP; ++c) br[c] = b_in(c);
-#pragma unroll
-      for (int j = 0; j < N; ++j) ar[j] = a_in(j);
-      st_row<PP, S>(Yl, r, br);
-      st_row<N, S>(Al, r, ar);
-    }
-    wave_sync();
-    double bc[N], tr[N];  // column r of B ; row r of T = B' P
-#pragma unroll
-    for (int l = 0; l < N; ++l) bc[l] = Yl[l * S + rp];
-    row_times<N, N, S>(bc, Hl, tr);
-    double w[PP + N];
-#pragma unroll
-    for (int c = 0; c < PP; ++c) {
-      double s = r_in(c);
-#pragma unroll
-      for (int l = 0; l < N; ++l) s += tr[l] * Yl[l * S + c];
-      w[c] = s;
-    }
-    row_times<N, N, S>(tr, Al, w + PP);
-    wave_sync();
-    int col;
-    if (!group_gauss_jordan<PP, PP + N, GS>(w, r, Tl, &col)) st = QT_DARE_SINGULAR;
-    if (st == QT_DARE_OK && col >= 0 && col < p) {
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (j < n) K[(int64_t)(col * n + j) * m + pb] = w[PP + j];
-    }
-  }
-  if (!valid) return;
-  const bool ok = st == QT_DARE_OK;
-  if (ok) {
-    if (P && r < n) {
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (j < n) P[(int64_t)(r * n + j) * m + pb] = Hl[r * S + j];
-    }
-  } else {
-    if (r < p) store_failed_gain_row<N>(r, n, p, m, pb, q, rin, fallback && hover, K);
-    if (P && r < n) {
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (j < n) P[(int64_t)(r * n + j) * m + pb] = 0.0;
-    }
-  }
-  // one status per problem (st is uniform over the group), from its first lane
-  if (r == 0) {
-    status[pb] = (int8_t)st;
-    if (iters) iters[pb] = it;
-  }
-}
-
 // ------------------------------------------------------- row kernel
 //
 // The same dense SDA with its products in registers.  One problem per DPP
@@ -850,9 +509,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_WAVE
 // sum_l X[r][l] Y[j][l]) broadcasts lane j instead.  LDS is left with what
 // moves data between lanes by a data-dependent or transposed pattern: the
 // inversion's pivot rows (the pivot lane is chosen at run time), the
-// inverse's row / column permutation, and three transposes per doubling
-// (A' for A' H Y1, and the two symmetrisations).  Validation, G = B R^-1 B'
-// and the final gain are the group kernel's code (once per problem).
+// inverse's row / column permutation (the pivoted fallback), and the
+// transposes (A' for A' H Y1; the symmetrisations with QT_DARE_SYM).
+// Validation, G = B R^-1 B' and the final gain are once per problem.
 
 // v_fmac_f64 with its first source broadcast from lane l of each DPP row
 // (row_newbcast: the DPP control gfx950 applies to 64-bit operands), N per
@@ -1032,11 +691,16 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
   return v;
 }
 
-// group_gj_invert for the row kernel (one problem per 16-lane DPP row): the
-// pivot is the row whose |w[k]| has the largest high word (exponent and the
-// top 20 mantissa bits: partial pivoting to 2^-20, ties to the lowest row),
-// found by a 32-bit DPP maximum, and the pivot row is scaled by a Newton
-// reciprocal.  Same in-place form and return values as group_gj_invert.
+// In-place Gauss-Jordan inversion with partial pivoting of the group's
+// NR x NR matrix W (one problem per 16-lane DPP row), row r in this lane's w
+// (lanes r >= NR hold no row).  Rows are not swapped: pk[k] records the lane
+// whose row became pivot k (the same in every lane of the group) and *col the
+// pivot this lane's row became; on return the lanes hold S with
+// W^-1[a][pk[k]] = S[pk[a]][k].  The pivot is the row whose |w[k]| has the
+// largest high word (exponent and the top 20 mantissa bits: partial pivoting
+// to 2^-20, ties to the lowest row), found by a 32-bit DPP maximum; the pivot
+// row is scaled by a Newton reciprocal and broadcast through `piv` (LDS).
+// Returns false (uniform over the group) when a pivot column is all zero.
 template <int NR>
 __device__ __forceinline__ bool row_gj_invert(double (&w)[NR], int r, double* piv, int (&pk)[NR], int* col) {
   bool used = r >= NR;
@@ -1083,8 +747,8 @@ __device__ __forceinline__ void lds_transpose(double* buf, const double (&row)[N
   wave_sync();
 }
 
-// 1: symmetrise H and G after every doubling, (M + M') / 2, as dare_group_kernel
-// does; 0: add M as computed (A' (H W^-1) A and A (W^-1 G) A' are symmetric in
+// 1: symmetrise H and G after every doubling, (M + M') / 2, as round 3's LDS
+// kernel did; 0: add M as computed (A' (H W^-1) A and A (W^-1 G) A' are symmetric in
 // exact arithmetic: H W^-1 = (I + H G)^-1 H), which spares two LDS transposes
 #ifndef QT_DARE_SYM
 #define QT_DARE_SYM 0
@@ -1152,7 +816,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     return (valid && r < p && c < p) ? rin[(int64_t)(r * p + c) * m + pb] : (r == c ? 1.0 : 0.0);
   };
 
-  // ---- validation (riccati_lqr.py:57-116), as in dare_group_kernel
+  // ---- validation (_is_positive_semidefinite / _is_positive_definite,
+  // riccati_lqr.py:57-116): symmetric within np.allclose, then the
+  // eigenvalue bounds as Cholesky tests: min eig(Q) >= -1e-10 <=> Q + 1e-10 I
+  // positive definite, min eig(R) > 1e-10 <=> R - 1e-10 I positive definite
+  // (the same decisions but on the boundary itself, to rounding)
   double hr[N];  // H = Q to start
 #pragma unroll
   for (int j = 0; j < N; ++j) hr[j] = (real && j < n) ? q[(int64_t)(r * n + j) * m + pb] : 0.0;
@@ -1173,7 +841,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     st = !qok ? QT_DARE_Q_NOT_PSD : (!rok ? QT_DARE_R_NOT_PD : QT_DARE_OK);
   }
 
-  // ---- G = B R^-1 B' (as in dare_group_kernel)
+  // ---- G = B R^-1 B': X = R^-1 B' by Gauss-Jordan on [R | B'] (lanes r < PP), G = B X
   double gr[N];
   int it = 0;
   bool conv = false;
@@ -1303,7 +971,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
   if (r < N) st_row<N, S>(Hl, r, hr);  // P for the gain phase and the output
   wave_sync();
 
-  // ---- K = (R + B'PB)^-1 B'PA (riccati_lqr.py:181-182), as in dare_group_kernel
+  // ---- K = (R + B'PB)^-1 B'PA (riccati_lqr.py:181-182): T = B'P (lanes r < PP),
+  // W = R + T B, Y = T A0, solve W K = Y
   if (valid && st == QT_DARE_OK) {
     if (r < N) {
       double br[PP], a0[N];
@@ -1351,40 +1020,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
   }
 }
 
-#ifndef QT_DARE_KERNEL
-#define QT_DARE_KERNEL 1  // 1: dare_row_kernel (DPP products), 0: dare_group_kernel (LDS products)
-#endif
-
 // Launch the dense kernel sized for (n, p): 6 / 4, 9 / 4, else 16 / 8.
-inline void launch_dare_group(int n, int p, int64_t m, const double* A, const double* B, int ab_per_problem,
+inline void launch_dare_dense(int n, int p, int64_t m, const double* A, const double* B, int ab_per_problem,
                               double dt, double gravity, const double* mass, const double* q, const double* r,
                               int fallback, double* K, double* P, int8_t* status, int32_t* iters, hipStream_t s) {
-  if (QT_DARE_KERNEL == 1) {
-    const int grid = (int)((m + 3) / 4);
-    if (n <= 6 && p <= 4)
-      dare_row_kernel<6, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K,
-                                                P, status, iters);
-    else if (n <= 9 && p <= 4)
-      dare_row_kernel<9, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K,
-                                                P, status, iters);
-    else
-      dare_row_kernel<16, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback,
-                                                 K, P, status, iters);
-    return;
-  }
-  if (n <= 6 && p <= 4) {
-    const int grid = (int)((m + 7) / 8);
-    dare_group_kernel<6, 4, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
-                                                   fallback, K, P, status, iters);
-  } else if (n <= 9 && p <= 4) {
-    const int grid = (int)((m + 3) / 4);
-    dare_group_kernel<9, 4, 16><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
-                                                    fallback, K, P, status, iters);
-  } else {
-    const int grid = (int)((m + 3) / 4);
-    dare_group_kernel<16, 8, 16><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r,
-                                                     fallback, K, P, status, iters);
-  }
+  const int grid = (int)((m + 3) / 4);
+  if (n <= 6 && p <= 4)
+    dare_row_kernel<6, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K, P,
+                                              status, iters);
+  else if (n <= 9 && p <= 4)
+    dare_row_kernel<9, 4><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K, P,
+                                              status, iters);
+  else
+    dare_row_kernel<16, 8><<<grid, 64, 0, s>>>(n, p, m, A, B, ab_per_problem, dt, gravity, mass, q, r, fallback, K,
+                                               P, status, iters);
 }
 
 }  // namespace
@@ -1405,7 +1054,7 @@ extern "C" int qt_dare_batched(int32_t n_state, int64_t m, double dt, double gra
       dare_axis_kernel<6><<<grid, 256, 0, s>>>(m, dt, gravity, mass, q, r, K, P, status, iters);
   } else {
     if (m > ((int64_t)0x7fffffff) * 4) return QT_EINVAL;
-    launch_dare_group(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r, 1, K, P, status, iters, s);
+    launch_dare_dense(n_state, 4, m, nullptr, nullptr, 0, dt, gravity, mass, q, r, 1, K, P, status, iters, s);
   }
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }
@@ -1416,7 +1065,7 @@ extern "C" int qt_dare_dense(int32_t n, int32_t p, int64_t m, const double* A, c
   if (n < 1 || n > kMaxN || p < 1 || p > kMaxP || m < 0 || m > ((int64_t)0x7fffffff) * 4) return QT_EINVAL;
   if (m == 0) return QT_OK;  // empty: no pointer is read
   if (!A || !B || !q || !r || !K || !status) return QT_EINVAL;
-  launch_dare_group(n, p, m, A, B, ab_per_problem, 0.0, 0.0, nullptr, q, r, 0, K, P, status, iters,
+  launch_dare_dense(n, p, m, A, B, ab_per_problem, 0.0, 0.0, nullptr, q, r, 0, K, P, status, iters,
                     (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ELAUNCH;
 }

@@ -609,6 +609,9 @@ __device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizo
 // runs it with the clamp in every step — exactly the voted step without the
 // vote, so results are bitwise those of the voted loop.
 constexpr int kDualBelow = 8;  // tilt-bounded horizons shorter than this try the clamping body
+#ifndef QT_GROUPED_DUAL
+#define QT_GROUPED_DUAL 0  // the grouped kernel (two waves per SIMD, 256 VGPRs) too
+#endif
 
 template <int MOTION, int KC, bool FF, bool KS, bool UNI, bool DUAL = false>
 __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
@@ -937,9 +940,10 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
 #endif
     if constexpr (FLAVOR == kYaw0)
       run_yaw0<MOTION, KC, FF, KS, UNI,
-               FRESH && KC != 9 && (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
-                                    MOTION == QT_MOTION_FIGURE8)>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ,
-                                                                  tg, t, a, nsteps, lc);
+               (FRESH || QT_GROUPED_DUAL) && KC != 9 &&
+                   (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
+                    MOTION == QT_MOTION_FIGURE8)>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
+                                                  lc);
     else
       run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec,
                                           n, ep);
