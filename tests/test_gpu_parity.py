@@ -628,8 +628,8 @@ def test_general_dare_random_systems(qt):
 
 @pytest.mark.parametrize("n,p", [(1, 1), (3, 8), (16, 1), (16, 8), (10, 6)])
 def test_dense_dare_batch_edge_sizes(qt, n, p):
-    """The dense group kernel at its size limits (n <= 16, p <= 8, every
-    group-size branch of launch_dare_group) on a ragged batch of 67 random
+    """The dense row kernel at its size limits (n <= 16, p <= 8, every
+    size branch of launch_dare_dense) on a ragged batch of 67 random
     problems (not a multiple of the problems per wave): every problem
     satisfies its own DARE and K = (R + B'PB)^-1 B'PA; sizes outside the
     limits are refused."""
