@@ -535,6 +535,9 @@ struct Horizon {
   // as the biased-exponent bits of t; elsewhere fl(t + dt) - t is the same
   // for every t of a binade (t is a multiple of its ulp).
   long long tie_exp_bits;
+  // run_yaw0's DUAL: a tilt-bounded horizon shorter than this tries the
+  // clamping no-vote body (kDualBelow; 0 never does, for the bitwise test)
+  int dual_below;
 };
 
 QT_HD Horizon make_horizon(const qt_env_params& e, const qt_ctrl_params& c, const RateLin& rl) {

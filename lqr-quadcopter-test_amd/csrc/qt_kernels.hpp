@@ -608,7 +608,7 @@ __device__ __forceinline__ int yaw0_horizon(const qt_env_params& e, const Horizo
 // a wave bounds its horizon without the tilt (speed, position, time only) and
 // runs it with the clamp in every step — exactly the voted step without the
 // vote, so results are bitwise those of the voted loop.
-constexpr int kDualBelow = 8;  // tilt-bounded horizons shorter than this try the clamping body
+constexpr int kDualBelow = 8;  // tilt-bounded horizons shorter than this try the clamping body (Horizon::dual_below)
 #ifndef QT_GROUPED_DUAL
 #define QT_GROUPED_DUAL 0  // the grouped kernel (two waves per SIMD, 256 VGPRs) too
 #endif
@@ -749,7 +749,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
       int H = yaw0_horizon<kTiltHorizon, kFold>(e, k.hz, lin, pl, x, t, rem);
       bool clamp_body = false;  // wave-uniform (H comes from ballots)
       if constexpr (DUAL) {
-        if (H < kDualBelow) {
+        if (H < k.hz.dual_below) {
           const int H2 = yaw0_horizon<false, kFold>(e, k.hz, lin, pl, x, t, rem);
           if (H2 > H) H = H2, clamp_body = true;
         }

@@ -582,6 +582,14 @@ unsigned long long* defer_flag_for(hipStream_t s) {
   return f;
 }
 
+// run_yaw0's DUAL threshold: kDualBelow, or QT_DUAL_BELOW from the environment
+// (a test knob: 0 turns the clamping no-vote body off, so a test can compare
+// the two loops' results bit for bit)
+int dual_below() {
+  const char* v = getenv("QT_DUAL_BELOW");
+  return v && *v ? atoi(v) : kDualBelow;
+}
+
 // The step flavour a launch can take (launch-level preconditions).
 int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
@@ -602,6 +610,7 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
                    double* met = nullptr) {
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   lc.hz = make_horizon(e, c, lc.rl);       // the yaw-at-rest loop's safe horizon
+  lc.hz.dual_below = dual_below();
   lc.reward = reward;
   lc.fresh_off = fresh_off, lc.met = met;  // qt_rollout_fresh: reset in the prologue, metrics in the epilogue
   const bool ks_eff = ks || kc == 3;

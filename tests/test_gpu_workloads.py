@@ -153,3 +153,25 @@ def test_batched_tuner_vs_sequential_oracle(qt, horizon):
         assert got["metrics"]["mean_on_target_ratio"] == pytest.approx(np.mean(list(ratio)), abs=1e-12)
         best = max(best, score)
     assert res.best_score == pytest.approx(best, rel=1e-9, abs=1e-9)
+
+
+def test_clamping_no_vote_body_is_bitwise_the_voted_loop(qt, monkeypatch):
+    """run_yaw0's DUAL body (a clamping no-vote horizon for waves whose
+    tilt-bounded horizon is short) against the same launches with it turned
+    off (QT_DUAL_BELOW=0: those waves take voted steps): every metric and the
+    final state bit for bit, on config-4 waves (tuner candidates, circular),
+    where a lane at the tilt clamp makes 46% of the steps voted without it."""
+    from quadtrack import workloads
+    from quadtrack.rollout import run_closed_loop
+
+    sh = workloads.build(4, 100000, 100000 + 2048)
+    res = []
+    for below in ("0", None):
+        if below is None:
+            monkeypatch.delenv("QT_DUAL_BELOW", raising=False)
+        else:
+            monkeypatch.setenv("QT_DUAL_BELOW", below)
+        r = run_closed_loop(sh.controller, **sh.run_kwargs())
+        res.append((r.metrics.clone(), r.state.x.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
