@@ -257,8 +257,12 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    yaw-at-rest fast flavour runs every group in ONE launch: each group starts
    at a 64-lane wave boundary, so every wave takes the loop specialised for its
    motion (<= 8 non-empty groups; more fall back to one launch per group);
-   other flavours launch once per group.  Results are identical to
-   qt_rollout's.  seg_motion must agree with batch->motion (when given) for
+   other flavours launch once per group.  seg_motion[i] == -1 marks a mixed
+   segment whose slots take each episode's motion from batch->motion (the
+   per-lane-motion loop); as the LAST segment it is the groups' remainders
+   packed into whole waves, launched on a second stream beside the grouped
+   launch and joined back to `stream` before return (core.motion_groups).
+   Results are identical to qt_rollout's.  seg_motion must agree with batch->motion (when given) for
    every slot; a wave holding a slot whose batch->motion differs is run by the
    exact pass, which takes each episode's motion from batch->motion. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,

@@ -913,7 +913,10 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   // leaves a wave holding a lane whose own motion differs (a caller's
   // inconsistent seg_motion, rollout_grouped_kernel) to this exact pass, which
   // reads the motion per lane
-  if (FLAVOR == kExact && b.nseg && b.motion) lane_ok = lane_ok && (int)b.motion[ep] == slot_motion(b, slot);
+  if (FLAVOR == kExact && b.nseg && b.motion) {
+    const int sm = slot_motion(b, slot);  // -1: the mixed tail segment, per-lane motion
+    lane_ok = lane_ok && (sm < 0 || (int)b.motion[ep] == sm);
+  }
   // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
   // never command yaw: a yaw at rest stays exactly zero
   // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
@@ -1015,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
   const int64_t slot = slot_at(b, p);
   if (slot < 0) return;
   const int wm = wave_motion(b, p);
-  if (b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
+  if (wm >= 0 && b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
     // a lane's own motion is not its group's: the exact pass runs the wave
     if (lc.defer_flag) *lc.defer_flag = lc.epoch;
     return;

@@ -9,6 +9,7 @@ batch's device.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -353,10 +354,23 @@ def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: Epi
               "qt_rollout_rewards")
 
 
+WAVE = 64  # lanes per wavefront: the grouped rollout starts every motion group at a wave boundary
+MIXED_TAIL = os.environ.get("QT_MIXED_TAIL", "1") != "0"  # A/B knob: 0 = one partial wave per motion
+
+
 def motion_groups(motion):
     """Grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end).
     A device tensor of motion types is grouped on the device (stable sort, one
-    5-element read back); a numpy array on the host."""
+    5-element read back); a numpy array on the host.
+
+    Every group starts at a wave boundary, so a group whose size is not a
+    multiple of 64 ends in a partly empty wave: up to one extra wave per
+    motion.  When two or more groups have such remainders, they are packed
+    instead into a mixed tail segment (seg_motion -1, the last one) after the
+    groups' whole waves, which qt_rollout_grouped runs with the per-lane-motion
+    loop beside the grouped launch: ceil(sum of remainders / 64) waves instead
+    of one per motion (config 5's 131,072-episode shard: 2,050 waves -> 2,045 + 3,
+    one round at two waves per SIMD instead of two)."""
     if isinstance(motion, torch.Tensor):
         m = motion.reshape(-1)
         order = torch.argsort(m, stable=True).to(torch.int32)
@@ -366,7 +380,21 @@ def motion_groups(motion):
         order = np.argsort(m, kind="stable").astype(np.int32)
         counts = np.bincount(m.astype(np.intp), minlength=5)  # motion types 0..4: O(n), no sort
     kinds = np.nonzero(counts)[0]
-    return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts[kinds])]
+    full = (counts // WAVE) * WAVE
+    rem = counts - full
+    if not MIXED_TAIL or np.count_nonzero(rem) < 2 or -(-int(rem.sum()) // WAVE) >= int(np.count_nonzero(rem)):
+        return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts[kinds])]
+    # slots: each motion's whole waves, then every motion's remainder (the mixed tail)
+    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    pieces = [(int(start[k]), int(full[k])) for k in kinds if full[k]] + \
+             [(int(start[k] + full[k]), int(rem[k])) for k in kinds if rem[k]]
+    if isinstance(order, torch.Tensor):
+        idx = torch.cat([torch.arange(a, a + c, device=order.device) for a, c in pieces])
+    else:
+        idx = np.concatenate([np.arange(a, a + c) for a, c in pieces])
+    seg_motion = [int(k) for k in kinds if full[k]] + [-1]
+    seg_end = [int(v) for v in np.cumsum([full[k] for k in kinds if full[k]])] + [int(counts.sum())]
+    return order[idx], seg_motion, seg_end
 
 
 def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:

@@ -3,7 +3,7 @@
 # secondary workloads: config 3 (LQI, sinusoidal), config 4 (per-episode Q/R,
 # circular: 262,144 episodes on one GPU, cfg4, and the 65,536-episode shard each
 # of its 4 GPUs runs, cfg4s), config 5 (1M episodes, grouped motions, one
-# launch), and the batched DARE kernels (scripts/dare_bench.py).  Every step is
+# launch; cfg5s: the 131,072-episode shard each of its 8 GPUs runs), and the batched DARE kernels (scripts/dare_bench.py).  Every step is
 # time-limited; the first failure ends the script.  Outputs under
 # gpurun_out/profw_<tag>/<case>_{trace,sq}/.
 set -e -o pipefail
@@ -33,6 +33,7 @@ for c in ${CASES:-cfg3 cfg5 dare}; do
     cfg4) run_case cfg4 scripts/run_workload.py --config 4 --repeat 5 ;;
     cfg4s) run_case cfg4s scripts/run_workload.py --config 4 --episodes 65536 --repeat 10 ;;
     cfg5) run_case cfg5 scripts/run_workload.py --config 5 --repeat 5 ;;
+    cfg5s) run_case cfg5s scripts/run_workload.py --config 5 --episodes 131072 --repeat 10 ;;
     dare) run_case dare scripts/dare_bench.py --reps 5 ${DARE_ARGS:-} ;;
   esac
 done

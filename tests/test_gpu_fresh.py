@@ -105,10 +105,12 @@ def test_fresh_pass_deferred_wave(qt):
     assert met[-1, 130] < 3000 and np.all(met[-1, :128] == 3000)
 
 
-def test_fresh_pass_grouped_mixed(qt):
+@pytest.mark.parametrize("n", [640, 700])
+def test_fresh_pass_grouped_mixed(qt, n):
+    """640: five groups of two whole waves; 700: 140 per motion, the 12-episode
+    remainders packed into a mixed tail (core.motion_groups)."""
     from quadtrack.controllers import BatchedRiccatiLQR
 
-    n = 640
     mass = np.random.default_rng(3).uniform(0.8, 1.2, n)
     motion = np.arange(n) % 5
     ctl = BatchedRiccatiLQR({"dt": 0.01}, mass=torch.as_tensor(mass, device="cuda"))

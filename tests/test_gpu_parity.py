@@ -485,7 +485,8 @@ def test_deferred_waves_run_exact_pass(qt):
 def test_mixed_motion_order_permutation(qt):
     """Mixed motion types: the per-step runtime-motion kernel, the same kernel
     under a permuting `order`, and the grouped motion-specialised launches
-    (qt_rollout_grouped, the default) give the same results: bitwise between
+    (qt_rollout_grouped, the default: the groups' whole waves in one launch, their
+    remainders in a mixed tail beside it) give the same results: bitwise between
     the first two; within 1e-9 for the grouped launches, whose circular and
     sinusoidal groups carry the target sin / cos across steps
     (target_state_carried) where the runtime-motion kernel evaluates them."""
@@ -503,7 +504,8 @@ def test_mixed_motion_order_permutation(qt):
     assert b.groups is None
     r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
     g = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
-    assert g.batch.groups is not None and len(g.batch.groups[0]) == 5
+    # 400 per motion: 6 whole waves each, the 16-episode remainders in a mixed tail
+    assert g.batch.groups is not None and list(g.batch.groups[0]) == [0, 1, 2, 3, 4, -1]
     assert torch.equal(a.metrics, r.metrics)
     assert torch.equal(a.state.x, r.state.x)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), g.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
