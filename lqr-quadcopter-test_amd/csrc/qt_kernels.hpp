@@ -1041,6 +1041,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
   }
 }
 
+// The mixed tail of a grouped batch (core.motion_groups: the groups'
+// remainders packed into whole waves, seg_motion -1): the runtime-motion
+// yaw-at-rest loop over slots [slot0, slot_end), at the grouped kernel's two
+// waves per SIMD.  It runs beside rollout_grouped_kernel on a second stream
+// (qt_rollout_grouped) and fills the slots the grouped waves leave; the
+// runtime-motion rollout_kernel (285 VGPRs) would take a whole SIMD per wave,
+// the register file of two grouped waves.
+template <int KC, bool FF, bool KS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUPED_WAVES))) void rollout_tail_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
+                                                                 BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
+  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
+  if (slot < 0) return;
+  rollout_lane<kYaw0, -1, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+}
+
 inline BatchDev to_dev(const qt_batch* b) {
   BatchDev d{};
   d.n = b->n, d.motion = b->motion, d.pattern = b->pattern, d.plant_mass = b->plant_mass;
@@ -1062,7 +1077,8 @@ inline bool valid_state(const qt_state& st, bool need_integ) {
 // (kFast or kYaw0) for the runtime controller / target choice.
 // uni: no per-episode mass, hover thrust or gains (rollout_kernel's UNI).
 // grouped: the yaw-at-rest flavour of a motion-grouped batch in one launch
-// (rollout_grouped_kernel; `motion` is ignored).
+// (rollout_grouped_kernel; `motion` is ignored), or with b.nseg == 0 its mixed tail
+// (rollout_tail_kernel).
 void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
                  const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
                  const qt_state& st, int nsteps, const LaunchConst& lc);

@@ -719,8 +719,9 @@ int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_crit
           ts = ss->s;
         else
           ss = nullptr;
+        // grouped with no segments: rollout_tail_kernel (two waves per SIMD, as the grouped waves)
         const int rt = launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, grid_of(bt.slot_end - bt.slot0), ts, e, c,
-                                      cr, bt, st, nsteps, rec);
+                                      cr, bt, st, nsteps, rec, true);
         if (ss && hipEventRecord(ss->join, ss->s) != hipSuccess) return QT_ELAUNCH;
         if (rt != QT_OK) return rt;
       }

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--ctl", default="lqr")
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--dump", default="", help="write the per-wave stamps to this .npz")
+    ap.add_argument("--workload", type=int, default=0,
+                    help="a BASELINE workload instead (quadtrack.workloads; 5: the grouped kernel, "
+                         "its first --n episodes; run with QT_MIXED_TAIL=0, whose one launch owns the stamps)")
     args = ap.parse_args()
     if "QUADTRACK_LIB" not in os.environ:
         os.environ["QUADTRACK_LIB"] = os.path.join(ROOT, "build", "stamp", "libquadtrack.so")
@@ -50,12 +53,24 @@ def main():
         raise SystemExit(f"{_abi.LIB_PATH} is not a -DQT_CLOCK_STAMP=1 build")
     lib.qt_debug_stamps.argtypes = [C.c_void_p, C.c_int64]
     dev = torch.device("cuda", 0)
-    cfg_c = {"dt": 0.01} if args.ctl == "lqr" else {"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]}
-    ctl = BatchedRiccatiLQR(cfg_c, device=dev)
-    cfg = EnvConfig.from_dict({"target": {"motion_type": args.motion}})
-    env = cfg.to_params()
     n = args.n
-    batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+    wave_motion = None
+    if args.workload:
+        from quadtrack import workloads
+
+        sh = workloads.build(args.workload, 0, n, device=dev)
+        ctl, cfg = sh.controller, sh.env_config
+        batch = build_batch(ctl, cfg, n, seeds=sh.seeds, motion=sh.motion, plant_mass=sh.plant_mass)
+        if batch.groups is not None:
+            batch, _ = batch.physical_groups()
+            wave_motion = np.concatenate([np.full(-(-(b - a) // 64), m) for m, a, b in
+                                          zip(batch.groups[0], [0] + list(batch.groups[1][:-1]), batch.groups[1])])
+    else:
+        cfg_c = {"dt": 0.01} if args.ctl == "lqr" else {"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]}
+        ctl = BatchedRiccatiLQR(cfg_c, device=dev)
+        cfg = EnvConfig.from_dict({"target": {"motion_type": args.motion}})
+        batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+    env = cfg.to_params()
     st = core.RolloutState.empty(n, dev)
     steps = max_steps_for(env)
     crit = core.criteria()
@@ -70,7 +85,7 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
-    waves = (n + 63) // 64
+    waves = (n + 63) // 64 if wave_motion is None else len(wave_motion)
     buf = np.zeros((waves, 6), dtype=np.uint64)
     _abi.check(lib.qt_debug_stamps(buf.ctypes.data, waves), "qt_debug_stamps")
     dt = (buf[:, 1] - buf[:, 0]).astype(np.float64)
@@ -102,6 +117,15 @@ def main():
     end = (buf[:, 3].astype(np.float64) - buf[:, 2].min()) / 1e5
     out["start_ms_p50_p99_max"] = [round(float(v), 4) for v in np.percentile(start, [50, 99, 100])]
     out["end_ms_p50_p99_max"] = [round(float(v), 4) for v in np.percentile(end, [50, 99, 100])]
+    if wave_motion is not None:  # per motion group: loop time, start and end (ms from the first start)
+        out["by_motion"] = {int(m): {"waves": int((wave_motion == m).sum()),
+                                     "loop_ms_median": round(float(np.median(dr[wave_motion == m])) / 1e5, 4),
+                                     "start_ms_max": round(float(start[wave_motion == m].max()), 4),
+                                     "end_ms_max": round(float(end[wave_motion == m].max()), 4)}
+                            for m in np.unique(wave_motion)}
+        late = start > 0.05
+        out["late_waves"] = int(late.sum())
+        out["late_start_ms_min"] = round(float(start[late].min()), 4) if late.any() else None
     if args.dump:
         np.savez(args.dump, stamps=buf)
     print(json.dumps(out), flush=True)
