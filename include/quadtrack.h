@@ -259,9 +259,7 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    motion (<= 8 non-empty groups; more fall back to one launch per group);
    other flavours launch once per group.  seg_motion[i] == -1 marks a mixed
    segment whose slots take each episode's motion from batch->motion (the
-   per-lane-motion loop); as the LAST segment it is the groups' remainders
-   packed into whole waves, launched on a second stream beside the grouped
-   launch and joined back to `stream` before return (core.motion_groups).
+   per-lane-motion loop); a batch with one takes one launch set per segment.
    Results are identical to qt_rollout's.  seg_motion must agree with batch->motion (when given) for
    every slot; a wave holding a slot whose batch->motion differs is run by the
    exact pass, which takes each episode's motion from batch->motion. */

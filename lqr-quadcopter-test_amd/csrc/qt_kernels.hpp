@@ -913,10 +913,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   // leaves a wave holding a lane whose own motion differs (a caller's
   // inconsistent seg_motion, rollout_grouped_kernel) to this exact pass, which
   // reads the motion per lane
-  if (FLAVOR == kExact && b.nseg && b.motion) {
-    const int sm = slot_motion(b, slot);  // -1: the mixed tail segment, per-lane motion
-    lane_ok = lane_ok && (sm < 0 || (int)b.motion[ep] == sm);
-  }
+  if (FLAVOR == kExact && b.nseg && b.motion) lane_ok = lane_ok && (int)b.motion[ep] == slot_motion(b, slot);
   // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
   // never command yaw: a yaw at rest stays exactly zero
   // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
@@ -1018,7 +1015,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
   const int64_t slot = slot_at(b, p);
   if (slot < 0) return;
   const int wm = wave_motion(b, p);
-  if (wm >= 0 && b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
+  if (b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
     // a lane's own motion is not its group's: the exact pass runs the wave
     if (lc.defer_flag) *lc.defer_flag = lc.epoch;
     return;
@@ -1039,21 +1036,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
     default:
       rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
   }
-}
-
-// The mixed tail of a grouped batch (core.motion_groups: the groups'
-// remainders packed into whole waves, seg_motion -1): the runtime-motion
-// yaw-at-rest loop over slots [slot0, slot_end), at the grouped kernel's two
-// waves per SIMD.  It runs beside rollout_grouped_kernel on a second stream
-// (qt_rollout_grouped) and fills the slots the grouped waves leave; the
-// runtime-motion rollout_kernel (285 VGPRs) would take a whole SIMD per wave,
-// the register file of two grouped waves.
-template <int KC, bool FF, bool KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUPED_WAVES))) void rollout_tail_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
-                                                                 BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
-  const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
-  if (slot < 0) return;
-  rollout_lane<kYaw0, -1, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
 }
 
 inline BatchDev to_dev(const qt_batch* b) {
@@ -1077,8 +1059,7 @@ inline bool valid_state(const qt_state& st, bool need_integ) {
 // (kFast or kYaw0) for the runtime controller / target choice.
 // uni: no per-episode mass, hover thrust or gains (rollout_kernel's UNI).
 // grouped: the yaw-at-rest flavour of a motion-grouped batch in one launch
-// (rollout_grouped_kernel; `motion` is ignored), or with b.nseg == 0 its mixed tail
-// (rollout_tail_kernel).
+// (rollout_grouped_kernel; `motion` is ignored).
 void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, int motion, int grid, hipStream_t s,
                  const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
                  const qt_state& st, int nsteps, const LaunchConst& lc);

@@ -582,38 +582,6 @@ unsigned long long* defer_flag_for(hipStream_t s) {
   return f;
 }
 
-// A second stream per (device, caller stream) for work that runs beside the
-// caller's launches — the grouped rollout's mixed tail — with the events of
-// its fork from and join to the caller's stream.  Created once, kept for the
-// process lifetime.  Null when it cannot be created (the work then runs on the
-// caller's stream, in order).
-struct SideStream {
-  hipStream_t s;
-  hipEvent_t fork, join;
-};
-
-SideStream* side_stream_for(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SideStream*> sides;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = sides.find({dev, s});
-  if (it != sides.end()) return it->second;
-  SideStream* ss = new SideStream{};
-  if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess) {
-    delete ss;
-    return sides[{dev, s}] = nullptr;
-  }
-  if (hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess) {
-    (void)hipStreamDestroy(ss->s);
-    delete ss;
-    return sides[{dev, s}] = nullptr;
-  }
-  return sides[{dev, s}] = ss;
-}
-
 // run_yaw0's DUAL threshold: kDualBelow, or QT_DUAL_BELOW from the environment
 // (a test knob: 0 turns the clamping no-vote body off, so a test can compare
 // the two loops' results bit for bit)
@@ -677,18 +645,18 @@ int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_crit
   if (nseg == 0)
     return launch_rollout(batch->k_cols, ff, ks, no_yaw, batch->motion ? -1 : e.motion, grid_of(batch->n), s, e, c,
                           cr, b, st, nsteps, rec, false, nullptr, fresh_off, met);
-  // a mixed tail (seg_motion -1, core.motion_groups): the last segment, the
-  // groups' remainders packed into whole waves
-  const bool tail = seg_motion[nseg - 1] < 0;
-  bool tail_last_only = true;
-  for (int32_t i = 0; i + 1 < nseg; ++i) tail_last_only = tail_last_only && seg_motion[i] >= 0;
-  if (tail_last_only && flavor_for(batch->k_cols, ks, no_yaw, e, c, rec) == kYaw0) {
+  // a mixed segment (seg_motion -1: per-lane motion) has no loop in the grouped
+  // kernel: such a batch takes one launch set per segment, the mixed ones with
+  // the runtime-motion loop
+  bool mixed = false;
+  for (int32_t i = 0; i < nseg; ++i) mixed = mixed || seg_motion[i] < 0;
+  if (!mixed && flavor_for(batch->k_cols, ks, no_yaw, e, c, rec) == kYaw0) {
     // every group in one launch, each starting at a wavefront boundary (BatchDev's
     // wave-aligned segments; both the fast kernel and its exact pass map slots so)
     BatchDev bg = b;
     int64_t waves = 0, prev_end = 0;
     bool fits = true;
-    for (int32_t i = 0; i < nseg - (tail ? 1 : 0) && fits; ++i) {
+    for (int32_t i = 0; i < nseg && fits; ++i) {
       const int64_t cnt = seg_end[i] - prev_end;
       prev_end = seg_end[i];
       if (cnt == 0) continue;
@@ -705,31 +673,8 @@ int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_crit
     if (fits) {
       // the grouped kernel has no fresh prologue / epilogue (rollout_lane's FRESH)
       if (fresh_off) reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(e, b, fresh_off, st);
-      // The mixed tail beside the grouped launch, on the side stream and launched
-      // first: its few waves take the slots the grouped waves leave, so the two
-      // fill the machine in one round (the tail as extra grouped waves would
-      // start a second round once the grouped launch exceeds the resident waves)
-      SideStream* ss = nullptr;
-      if (tail && seg_end[nseg - 1] > prev_end) {
-        BatchDev bt = b;
-        bt.slot0 = prev_end, bt.slot_end = seg_end[nseg - 1];
-        ss = side_stream_for(s);
-        hipStream_t ts = s;
-        if (ss && hipEventRecord(ss->fork, s) == hipSuccess && hipStreamWaitEvent(ss->s, ss->fork, 0) == hipSuccess)
-          ts = ss->s;
-        else
-          ss = nullptr;
-        // grouped with no segments: rollout_tail_kernel (two waves per SIMD, as the grouped waves)
-        const int rt = launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, grid_of(bt.slot_end - bt.slot0), ts, e, c,
-                                      cr, bt, st, nsteps, rec, true);
-        if (ss && hipEventRecord(ss->join, ss->s) != hipSuccess) return QT_ELAUNCH;
-        if (rt != QT_OK) return rt;
-      }
-      int rc = QT_OK;
-      if (bg.nseg)
-        rc = launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, (int)((waves * 64 + kBlock - 1) / kBlock), s, e, c, cr,
-                            bg, st, nsteps, rec, true);
-      if (ss && hipStreamWaitEvent(s, ss->join, 0) != hipSuccess) return QT_ELAUNCH;
+      const int rc = launch_rollout(batch->k_cols, ff, ks, no_yaw, -1, (int)((waves * 64 + kBlock - 1) / kBlock), s,
+                                    e, c, cr, bg, st, nsteps, rec, true);
       if (rc != QT_OK || !met) return rc;
       metrics_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(cr, batch->n, st.acc, st.t, met);
       return check_launch();

@@ -47,12 +47,8 @@ struct GroupedLaunch {
   template <int MOTION, int KC, bool FF, bool KS>
   static void run(int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                   const BatchDev& b, const qt_state& st, int nsteps, const LaunchConst& lc) {
-    if constexpr (MOTION == -1) {  // one kernel per (KC, FF, KS): instantiated through the runtime-motion slot only
-      if (b.nseg)
-        rollout_grouped_kernel<KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
-      else  // a grouped batch's mixed tail (slot range, no segments)
-        rollout_tail_kernel<KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
-    }
+    if constexpr (MOTION == -1)  // one kernel per (KC, FF, KS): instantiated through the runtime-motion slot only
+      rollout_grouped_kernel<KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
   }
 };
 

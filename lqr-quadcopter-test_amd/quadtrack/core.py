@@ -354,47 +354,35 @@ def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: Epi
               "qt_rollout_rewards")
 
 
-WAVE = 64  # lanes per wavefront: the grouped rollout starts every motion group at a wave boundary
-MIXED_TAIL = os.environ.get("QT_MIXED_TAIL", "1") != "0"  # A/B knob: 0 = one partial wave per motion
+# Slot order of the motion groups in a grouped rollout: longest wave first
+# (sinusoidal, figure-8, circular, linear, stationary: the per-motion loops'
+# wave times in config 5, profiles/r04/cfg5_stamps.json), so that the long
+# waves start first and the short ones fill the end of the launch (config 5:
+# 131,072 episodes 4.35 -> 3.93 ms, 1,048,576 23.5 -> 23.1 ms,
+# profiles/r04/grouping_ab.jsonl).  QT_GROUP_ORDER (a comma list of the five
+# motion types) is an A/B knob.
+GROUP_ORDER = tuple(int(v) for v in os.environ.get("QT_GROUP_ORDER", "3,4,2,1,0").split(","))
 
 
 def motion_groups(motion):
     """Grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end).
     A device tensor of motion types is grouped on the device (stable sort, one
-    5-element read back); a numpy array on the host.
-
-    Every group starts at a wave boundary, so a group whose size is not a
-    multiple of 64 ends in a partly empty wave: up to one extra wave per
-    motion.  When two or more groups have such remainders, they are packed
-    instead into a mixed tail segment (seg_motion -1, the last one) after the
-    groups' whole waves, which qt_rollout_grouped runs with the per-lane-motion
-    loop beside the grouped launch: ceil(sum of remainders / 64) waves instead
-    of one per motion (config 5's 131,072-episode shard: 2,050 waves -> 2,045 + 3,
-    one round at two waves per SIMD instead of two)."""
+    5-element read back); a numpy array on the host.  Groups follow
+    GROUP_ORDER; within a group, episodes keep their index order."""
+    if sorted(GROUP_ORDER) != [0, 1, 2, 3, 4]:
+        raise ValueError(f"GROUP_ORDER {GROUP_ORDER} is not an order of the motion types 0..4")
+    pos = np.empty(5, np.int64)
+    pos[list(GROUP_ORDER)] = np.arange(5)
     if isinstance(motion, torch.Tensor):
-        m = motion.reshape(-1)
-        order = torch.argsort(m, stable=True).to(torch.int32)
-        counts = torch.bincount(m.to(torch.int64), minlength=5).cpu().numpy()
+        m = motion.reshape(-1).to(torch.int64)
+        order = torch.argsort(torch.as_tensor(pos, device=m.device)[m], stable=True).to(torch.int32)
+        counts = torch.bincount(m, minlength=5).cpu().numpy()
     else:
-        m = np.asarray(motion).reshape(-1)
-        order = np.argsort(m, kind="stable").astype(np.int32)
-        counts = np.bincount(m.astype(np.intp), minlength=5)  # motion types 0..4: O(n), no sort
-    kinds = np.nonzero(counts)[0]
-    full = (counts // WAVE) * WAVE
-    rem = counts - full
-    if not MIXED_TAIL or np.count_nonzero(rem) < 2 or -(-int(rem.sum()) // WAVE) >= int(np.count_nonzero(rem)):
-        return order, [int(k) for k in kinds], [int(v) for v in np.cumsum(counts[kinds])]
-    # slots: each motion's whole waves, then every motion's remainder (the mixed tail)
-    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
-    pieces = [(int(start[k]), int(full[k])) for k in kinds if full[k]] + \
-             [(int(start[k] + full[k]), int(rem[k])) for k in kinds if rem[k]]
-    if isinstance(order, torch.Tensor):
-        idx = torch.cat([torch.arange(a, a + c, device=order.device) for a, c in pieces])
-    else:
-        idx = np.concatenate([np.arange(a, a + c) for a, c in pieces])
-    seg_motion = [int(k) for k in kinds if full[k]] + [-1]
-    seg_end = [int(v) for v in np.cumsum([full[k] for k in kinds if full[k]])] + [int(counts.sum())]
-    return order[idx], seg_motion, seg_end
+        m = np.asarray(motion).reshape(-1).astype(np.intp)
+        order = np.argsort(pos[m], kind="stable").astype(np.int32)
+        counts = np.bincount(m, minlength=5)  # motion types 0..4: O(n), no sort
+    kinds = [k for k in GROUP_ORDER if counts[k]]
+    return order, kinds, [int(v) for v in np.cumsum(counts[kinds])]
 
 
 def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:

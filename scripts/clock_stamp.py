@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--dump", default="", help="write the per-wave stamps to this .npz")
     ap.add_argument("--workload", type=int, default=0,
                     help="a BASELINE workload instead (quadtrack.workloads; 5: the grouped kernel, "
-                         "its first --n episodes; run with QT_MIXED_TAIL=0, whose one launch owns the stamps)")
+                         "its first --n episodes)")
     args = ap.parse_args()
     if "QUADTRACK_LIB" not in os.environ:
         os.environ["QUADTRACK_LIB"] = os.path.join(ROOT, "build", "stamp", "libquadtrack.so")

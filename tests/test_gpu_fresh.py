@@ -107,8 +107,8 @@ def test_fresh_pass_deferred_wave(qt):
 
 @pytest.mark.parametrize("n", [640, 700])
 def test_fresh_pass_grouped_mixed(qt, n):
-    """640: five groups of two whole waves; 700: 140 per motion, the 12-episode
-    remainders packed into a mixed tail (core.motion_groups)."""
+    """640: five groups of two whole waves; 700: 140 per motion, each group
+    ending in a partly empty wave."""
     from quadtrack.controllers import BatchedRiccatiLQR
 
     mass = np.random.default_rng(3).uniform(0.8, 1.2, n)

@@ -485,11 +485,11 @@ def test_deferred_waves_run_exact_pass(qt):
 def test_mixed_motion_order_permutation(qt):
     """Mixed motion types: the per-step runtime-motion kernel, the same kernel
     under a permuting `order`, and the grouped motion-specialised launches
-    (qt_rollout_grouped, the default: the groups' whole waves in one launch, their
-    remainders in a mixed tail beside it) give the same results: bitwise between
+    (qt_rollout_grouped, the default) give the same results: bitwise between
     the first two; within 1e-9 for the grouped launches, whose circular and
     sinusoidal groups carry the target sin / cos across steps
     (target_state_carried) where the runtime-motion kernel evaluates them."""
+    from quadtrack import core
     from quadtrack.controllers import BatchedRiccatiLQR
     from quadtrack.rollout import build_batch, run_closed_loop
 
@@ -504,8 +504,7 @@ def test_mixed_motion_order_permutation(qt):
     assert b.groups is None
     r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
     g = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
-    # 400 per motion: 6 whole waves each, the 16-episode remainders in a mixed tail
-    assert g.batch.groups is not None and list(g.batch.groups[0]) == [0, 1, 2, 3, 4, -1]
+    assert g.batch.groups is not None and list(g.batch.groups[0]) == list(core.GROUP_ORDER)
     assert torch.equal(a.metrics, r.metrics)
     assert torch.equal(a.state.x, r.state.x)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), g.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
@@ -533,6 +532,29 @@ def test_grouped_seg_motion_mismatch_runs_exact(qt):
     sm[1], sm[2] = sm[2], sm[1]
     bad = dataclasses.replace(g, groups=(sm, list(se)))
     r = run_closed_loop(ctl, {}, n=n, batch=bad, max_steps=400)
+    np.testing.assert_allclose(a.metrics.cpu().numpy(), r.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(a.state.x.cpu().numpy(), r.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
+
+
+def test_grouped_mixed_segment(qt):
+    """qt_rollout_grouped with a mixed segment (seg_motion -1: each episode's
+    motion from batch.motion) between two motion groups: one launch set per
+    segment, the mixed one with the runtime-motion loop; the same results as
+    the per-lane-motion run of the whole batch."""
+    import dataclasses
+
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch, run_closed_loop
+
+    n = 1000
+    motion = [i % 5 for i in range(n)]
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    plain = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, group_motion=False)
+    a = run_closed_loop(ctl, {}, n=n, batch=plain, max_steps=400)
+    g = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion)
+    sm, se = list(g.groups[0]), list(g.groups[1])
+    mixed = dataclasses.replace(g, groups=([sm[0], -1, sm[-1]], [se[0], se[-2], se[-1]]))
+    r = run_closed_loop(ctl, {}, n=n, batch=mixed, max_steps=400)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), r.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(a.state.x.cpu().numpy(), r.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
 

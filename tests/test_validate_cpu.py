@@ -41,41 +41,21 @@ def test_physical_groups_checks_order(order, msg):
         b.physical_groups()
 
 
-def _check_groups(m, order, seg_motion, seg_end):
-    import numpy as np
 
-    o = np.asarray(order.cpu() if isinstance(order, torch.Tensor) else order)
-    assert sorted(o.tolist()) == list(range(m.size))
-    starts = [0] + list(seg_end[:-1])
-    for k, a, b in zip(seg_motion, starts, seg_end):
-        if k >= 0:
-            assert np.all(m[o[a:b]] == k)
-            if seg_motion[-1] == -1:
-                assert (b - a) % core.WAVE == 0
-    assert seg_end[-1] == m.size
-    assert all(k >= 0 for k in seg_motion[:-1])
-
-
-@pytest.mark.parametrize("counts,tail", [((640, 128, 0, 64, 192), False),   # whole waves only
-                                         ((400, 400, 400, 400, 400), True),  # 5 remainders of 16: 2 tail waves
-                                         ((65, 0, 0, 0, 0), False),          # one motion
-                                         ((70, 70, 0, 0, 0), True),          # 2 remainders of 6 -> 1 wave: packed
-                                         ((100, 60, 0, 0, 0), False),        # 36 + 60 -> 2 waves: no gain
-                                         ((26215, 26214, 26214, 26214, 26214), True)])
-def test_motion_groups_layout(counts, tail):
-    """core.motion_groups: stable per-motion groups; when the groups'
-    remainders pack into fewer waves than one per motion, each group keeps
-    its whole waves and the remainders form a mixed tail (seg_motion -1,
-    last).  numpy and torch inputs give the same grouping."""
+@pytest.mark.parametrize("counts", [(640, 128, 0, 64, 192), (400, 400, 400, 400, 400), (65, 0, 0, 0, 0),
+                                    (0, 70, 70, 0, 0), (26215, 26215, 26214, 26214, 26214)])
+def test_motion_groups_layout(counts):
+    """core.motion_groups: one segment per motion present, in GROUP_ORDER
+    (longest wave first), each holding exactly that motion's episodes in index
+    order; numpy and torch inputs give the same grouping."""
     import numpy as np
 
     m = np.concatenate([np.full(c, k, np.int8) for k, c in enumerate(counts)])
     m = m[np.random.default_rng(0).permutation(m.size)]
     order, sm, se = core.motion_groups(m)
-    _check_groups(m, order, sm, se)
+    assert sm == [k for k in core.GROUP_ORDER if counts[k]]
+    assert se[-1] == m.size and sorted(order.tolist()) == list(range(m.size))
+    for k, a, b in zip(sm, [0] + se[:-1], se):
+        assert np.array_equal(order[a:b], np.nonzero(m == k)[0])
     to, tsm, tse = core.motion_groups(torch.as_tensor(m))
-    assert np.array_equal(np.asarray(to), order) and tsm == sm and tse == se
-    assert (sm[-1] == -1) == tail
-    if sm[-1] == -1:
-        rem = sum(c % core.WAVE for c in counts)
-        assert se[-1] - (se[-2] if len(se) > 1 else 0) == rem
+    assert np.array_equal(to.numpy(), order) and tsm == sm and tse == se
