@@ -260,9 +260,12 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    other flavours launch once per group.  seg_motion[i] == -1 marks a mixed
    segment whose slots take each episode's motion from batch->motion (the
    per-lane-motion loop); a batch with one takes one launch set per segment.
-   Results are identical to qt_rollout's.  seg_motion must agree with batch->motion (when given) for
-   every slot; a wave holding a slot whose batch->motion differs is run by the
-   exact pass, which takes each episode's motion from batch->motion. */
+   Results are qt_rollout's: bit for bit with 6-column gains; with 9-column
+   (LQI) gains within ~1e-10, where the specialised loops fold a periodic
+   target's carried rotor once per horizon.  seg_motion must agree with
+   batch->motion (when given) for every slot; a wave holding a slot whose
+   batch->motion differs is run by the exact pass, which takes each episode's
+   motion from batch->motion. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);
