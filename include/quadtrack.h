@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QT_ABI_VERSION 8
+#define QT_ABI_VERSION 9
 
 /* error codes */
 #define QT_OK 0
@@ -176,6 +176,60 @@ typedef struct qt_state {
   double* target;     /* [9][n] target p,v,a at t (the observation the controller sees next) */
 } qt_state;
 
+/* ABI 9.  A strided [rows][n] view of FP64 device memory: element (row r,
+   episode e) at p[r * rs + e * es].  A torch tensor of shape [n, k] is the view
+   {data_ptr, stride(1), stride(0)}: a contiguous [n, k] array (es = k, rs = 1)
+   and the [n, k] transpose of a [k][n] SoA array (es = 1, rs = n) both pass
+   without a copy. */
+typedef struct qt_view {
+  double* p;
+  int64_t rs, es;
+} qt_view;
+
+/* ABI 9.  The observation the controller reads (QuadcopterEnv._get_observation,
+   quadcopter_env.py:472-496): quadcopter position / velocity and target
+   position / velocity / acceleration, [3][n] each, and the observation time
+   (row 0 of `time`; PIDController only, controllers/__init__.py:262-265).
+   tacc.p and time.p may be NULL (zeros / unused). */
+typedef struct qt_obs_view {
+  qt_view pos, vel, tpos, tvel, tacc, time;
+} qt_obs_view;
+
+/* ABI 9.  Observation frame: what one batched env.step returns
+   (quadcopter_env.py:152-232) for every episode, in ONE contiguous device
+   block of QT_FRAME_BYTES(n) bytes (8-byte aligned):
+     double  f[QT_FR_ROWS][n]   rows below (state, target observation, info floats)
+     int64_t c[QT_FC_ROWS][n]   info counters
+     int8_t  b[QT_FB_ROWS][n]   done / info flags (0 or 1) and the termination code
+   A frame is written once by the launch that produces it and only read after:
+   the per-step entry points read the previous step's frame and write a new
+   one, so a frame the caller keeps (the observation of step k) never changes
+   (the reference's observation arrays are fresh copies, 481-486). */
+enum qt_frame_row {
+  QT_FR_X = 0,            /* 12 rows: px py pz vx vy vz roll pitch yaw p q r (quadcopter_env.py:63-70) */
+  QT_FR_TARGET = 12,      /* 9 rows: target position, velocity, clamped acceleration at `time` */
+  QT_FR_TIME = 21,        /* env time, t += dt (quadcopter_env.py:191) */
+  QT_FR_ERR = 22,         /* info["tracking_error"], post-step ||p - p_T|| (498-502) */
+  QT_FR_REWARD = 23,      /* reward = -tracking error (504-511) */
+  QT_FR_RATIO = 24,       /* info["on_target_ratio"] (215-219) */
+  QT_FR_ROWS = 25
+};
+enum qt_frame_count {
+  QT_FC_STEP = 0,         /* info["step"] */
+  QT_FC_VIOLATIONS,       /* info["action_violations"]: steps with a violation record (174-181) */
+  QT_FC_ON_TARGET,        /* env on-target count (205-207) */
+  QT_FC_ROWS
+};
+enum qt_frame_flag {
+  QT_FB_DONE = 0,         /* done (513-535) */
+  QT_FB_ON_TARGET,        /* info["on_target"] */
+  QT_FB_VIOLATION,        /* this step's action had a violation */
+  QT_FB_SUCCESS,          /* info["success"] (_evaluate_success, 537-553; the reference reports it when done) */
+  QT_FB_TERM,             /* enum qt_term: info["termination_reason"] */
+  QT_FB_ROWS
+};
+#define QT_FRAME_BYTES(n) ((int64_t)(n) * (QT_FR_ROWS * 8 + QT_FC_ROWS * 8 + QT_FB_ROWS))
+
 /* ---------------------------------------------------------------- entry points */
 
 /* ABI version of the loaded library. */
@@ -306,6 +360,45 @@ int qt_env_step(const qt_env_params* env, const qt_batch* batch, const double* a
    diag[18][n]: p, i, d, ff_velocity, ff_acceleration terms, total correction. */
 int qt_compute_action(const qt_ctrl_params* ctrl, const qt_batch* batch, const double* obs,
                       double* integ, double* action, int8_t* saturated, double* diag, void* stream);
+
+/* ---- ABI 9: the per-step API (one launch per step) ------------------------
+   The batched counterparts of the reference's step-at-a-time plugin calls,
+   for callers that drive the loop themselves (BatchedQuadcopterEnv.step,
+   Batched*.compute_action).  Episodes are in index order (batch->order must
+   be NULL).  Frames: QT_FRAME_BYTES(n) device blocks (qt_frame_row above). */
+
+/* QuadcopterEnv.reset(seed) (quadcopter_env.py:111-150) into a frame:
+   x = [p_target(0) + offset, 0...], target observation at t = 0, counters
+   and flags 0, tracking error / reward of the reset state. */
+int qt_frame_reset(const qt_env_params* env, const qt_batch* batch, const double* offset, void* frame,
+                   void* stream);
+
+/* QuadcopterEnv.step(action) (quadcopter_env.py:152-293) for every episode:
+   reads the state, time and counters of frame `in`, the action view ([4][n]:
+   thrust, roll, pitch, yaw rate; NaN / Inf zeroed and clipped as
+   _parse_and_validate_action), and writes frame `out` (in == out allowed).
+   freeze_done != 0: an episode whose `in` frame is done is not stepped (its
+   frame is carried over), as the Evaluator stops at done (eval.py:119-165);
+   0: it is stepped, as the reference's env does after done. */
+int qt_frame_step(const qt_env_params* env, const qt_batch* batch, const void* in, qt_view action, void* out,
+                  int32_t freeze_done, void* stream);
+
+/* compute_action on an observation view (RiccatiLQRController.compute_action,
+   riccati_lqr.py:779-967; k_cols 6 with heuristic gains: LQRController,
+   controllers/__init__.py:576-690; k_cols 3: PIDController, 243-379, with
+   obs->time).  integ as qt_compute_action (LQI [3][n], PID [4][n]) is read and
+   updated; action[4][n] and saturated[n] (may be NULL) are written. */
+int qt_compute_action_obs(const qt_ctrl_params* ctrl, const qt_batch* batch, const qt_obs_view* obs,
+                          double* integ, double* action, int8_t* saturated, void* stream);
+
+/* One closed-loop step in one launch: compute_action on frame `in`'s
+   observation (integ updated), then env.step with that action into frame
+   `out` (in == out allowed).  action[4][n] (may be NULL) receives the
+   controller's command.  freeze_done as qt_frame_step; a frozen episode's
+   controller state is not advanced either and its action row is 0. */
+int qt_frame_closed_step(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_batch* batch,
+                         const void* in, double* integ, void* out, double* action, int32_t freeze_done,
+                         void* stream);
 
 /* TargetMotion.get_state(t) (target_motion.py:387-411) for every episode at
    per-episode times t[n]: out[9][n] = position, velocity, clamped acceleration. */

@@ -15,7 +15,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # QUADTRACK_LIB points timing experiments (scripts/ablate.sh) at another build
 LIB_PATH = os.environ.get("QUADTRACK_LIB") or os.path.join(_HERE, "_lib", "libquadtrack.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # enums (include/quadtrack.h)
 MOTIONS = ("stationary", "linear", "circular", "sinusoidal", "figure8")
@@ -79,10 +79,35 @@ class State(C.Structure):
                 ("target", C.c_void_p)]
 
 
+class View(C.Structure):
+    """qt_view (ABI 9): element (row r, episode e) at p[r * rs + e * es]"""
+
+    _fields_ = [("p", C.c_void_p), ("rs", C.c_int64), ("es", C.c_int64)]
+
+
+class ObsView(C.Structure):
+    """qt_obs_view (ABI 9)"""
+
+    _fields_ = [(k, View) for k in ("pos", "vel", "tpos", "tvel", "tacc", "time")]
+
+
+# observation frame (qt_frame_row / qt_frame_count / qt_frame_flag, ABI 9)
+FR_ROWS, FC_ROWS, FB_ROWS = 25, 3, 5
+FR_X, FR_TARGET, FR_TIME, FR_ERR, FR_REWARD, FR_RATIO = 0, 12, 21, 22, 23, 24
+FC_STEP, FC_VIOLATIONS, FC_ON_TARGET = range(FC_ROWS)
+FB_DONE, FB_ON_TARGET, FB_VIOLATION, FB_SUCCESS, FB_TERM = range(FB_ROWS)
+
+
+def frame_bytes(n: int) -> int:
+    """QT_FRAME_BYTES(n)"""
+    return n * (FR_ROWS * 8 + FC_ROWS * 8 + FB_ROWS)
+
+
 EXPORTS = ("qt_abi_version", "qt_host_alloc", "qt_host_free", "qt_stream_sync", "qt_seed_draws", "qt_seed_uniform", "qt_reset", "qt_rollout", "qt_rollout_rewards", "qt_rollout_grouped", "qt_rollout_fresh",
            "qt_env_step", "qt_compute_action", "qt_target_state",
            "qt_episode_metrics", "qt_metrics_from_arrays", "qt_dare_batched", "qt_dare_dense", "qt_summary",
-           "qt_summary_parts", "qt_summary_numpy", "qt_stream_uniform")
+           "qt_summary_parts", "qt_summary_numpy", "qt_stream_uniform", "qt_frame_reset", "qt_frame_step",
+           "qt_compute_action_obs", "qt_frame_closed_step")
 
 _lib = None
 
@@ -125,6 +150,10 @@ def load():
     L.qt_summary_parts.argtypes = [i64, vp, dbl, dbl, vp, vp, i32, vp]
     L.qt_summary_numpy.argtypes = [i64, vp, i32, dbl, dbl, vp, vp]
     L.qt_stream_uniform.argtypes = [C.c_uint64, i64, i64, i32, vp, vp, vp, vp]
+    L.qt_frame_reset.argtypes = [P(EnvParams), P(Batch), vp, vp, vp]
+    L.qt_frame_step.argtypes = [P(EnvParams), P(Batch), vp, View, vp, i32, vp]
+    L.qt_compute_action_obs.argtypes = [P(CtrlParams), P(Batch), P(ObsView), vp, vp, vp, vp]
+    L.qt_frame_closed_step.argtypes = [P(EnvParams), P(CtrlParams), P(Batch), vp, vp, vp, vp, i32, vp]
     for name in EXPORTS[1:]:
         getattr(L, name).restype = C.c_int
     v = L.qt_abi_version()
@@ -152,6 +181,19 @@ def ptr(t: torch.Tensor | None):
 
 def stream_of(dev: torch.device):
     return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+try:  # the current stream's handle without building a torch.cuda.Stream object (per-step calls)
+    _raw_stream = torch._C._cuda_getCurrentRawStream
+except AttributeError:  # pragma: no cover
+    _raw_stream = None
+
+
+def raw_stream(dev: torch.device) -> int:
+    """stream_of as a plain int (the per-step API's hot path)."""
+    if _raw_stream is not None:
+        return _raw_stream(dev.index)
+    return torch.cuda.current_stream(dev).cuda_stream
 
 
 def check(rc: int, what: str):

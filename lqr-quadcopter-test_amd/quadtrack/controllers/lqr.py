@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from .. import _abi, core
+from ..step import BatchedControlMixin
 from .base import BaseController
 from .riccati_lqr import _OneEpisodeKernel, _ensure_array, _obs15, _validate_observation, ctrl_params
 
@@ -80,7 +81,7 @@ class LQRController(BaseController):
         return BatchedLQR({**self.config, "K": self.K}, device=device or self._kernel.dev)
 
 
-class BatchedLQR:
+class BatchedLQR(BatchedControlMixin):
     """Heuristic-LQR gains (LQRController, __init__.py:398-700) for a batch of
     episodes, for the fused closed loop (6-column K, no integral).  Shared, or
     per episode when any of q_pos / q_vel [n, 3], r_thrust / r_rate [n],
@@ -157,4 +158,5 @@ class BatchedLQR:
         out.ff = rep(self.ff)
         out.num_problems = self.num_problems * k
         out.per_episode = True
+        out.integral_state = None
         return out

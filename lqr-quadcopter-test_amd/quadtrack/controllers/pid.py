@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .. import _abi, core
+from ..step import BatchedControlMixin
 from .base import BaseController
 from .riccati_lqr import _OneEpisodeKernel, _ensure_array, _obs15, _validate_observation, ctrl_params
 
@@ -93,7 +94,7 @@ class PIDController(BaseController):
         return BatchedPID(self.config, device=device or self._kernel.dev)
 
 
-class BatchedPID:
+class BatchedPID(BatchedControlMixin):
     """PID gains for a batch of episodes (shared, or per episode when any of
     kp_pos / ki_pos / kd_pos [n, 3] or mass [n] is given), for the fused
     closed loop.  Each episode starts from a fresh controller (integral 0,
@@ -160,4 +161,5 @@ class BatchedPID:
         out.ff = rep(self.ff)
         out.num_problems = self.num_problems * k
         out.per_episode = True
+        out.integral_state = None
         return out

@@ -22,6 +22,7 @@ import torch
 
 from .. import _abi, core
 from .._abi import DARE_NO_CONVERGE, DARE_OK, DARE_Q_NOT_PSD, DARE_R_NOT_PD, CtrlParams
+from ..step import BatchedControlMixin
 from .base import BaseController
 
 logger = logging.getLogger(__name__)
@@ -429,7 +430,7 @@ class RiccatiLQRController(BaseController):
 # ----------------------------------------------------------- batched gains
 
 
-class BatchedRiccatiLQR:
+class BatchedRiccatiLQR(BatchedControlMixin):
     """Per-episode (or shared) Riccati-LQR / LQI gains on the GPU.
 
     `config` holds the shared options (the RiccatiLQRController keys).  Any of
@@ -578,20 +579,3 @@ class BatchedRiccatiLQR:
         out.integral_state = None
         return out
 
-    def reset(self, n: int | None = None) -> None:
-        n = n or self.num_problems
-        self.integral_state = torch.zeros(3, n, dtype=F64, device=self.device)
-
-    def compute_action(self, obs: dict) -> torch.Tensor:
-        """Batched compute_action on tensors: obs from BatchedQuadcopterEnv
-        ([n,3] tensors).  Returns actions [n, 4]; keeps the LQI integral."""
-        q, t = obs["quadcopter"], obs["target"]
-        n = q["position"].shape[0]
-        if self.per_episode and n != self.num_problems:
-            raise ValueError(f"{n} observations for {self.num_problems} per-episode gain sets")
-        o = torch.cat([q["position"], q["velocity"], t["position"], t["velocity"],
-                       t.get("acceleration", torch.zeros_like(t["position"]))], dim=1).T.contiguous()
-        if self.integral_state is None or self.integral_state.shape[1] != n:
-            self.reset(n)
-        act, _ = core.compute_action(self.ctrl, self.K, self.k_cols, o, self.integral_state, self.hover, ff=self.ff)
-        return act.T.contiguous()

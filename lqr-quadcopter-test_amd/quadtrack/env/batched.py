@@ -1,22 +1,37 @@
 """Batched quadcopter environment on the GPU.
 
-`BatchedQuadcopterEnv(n, config)` holds n independent episodes in HBM
-(structure-of-arrays float64) and exposes the reference's reset/step API
-(env/quadcopter_env.py:111-232) on tensors: `reset(seeds)` runs the reset
-kernel on the per-seed draws, `step(actions)` runs the open-loop step kernel
-(action validation, RK4/Euler, state constraints, post-step tracking error,
-termination) for every episode at once.  Returned tensors are fresh copies
-owned by the caller, like the reference's observation arrays
-(quadcopter_env.py:481-486).
+`BatchedQuadcopterEnv(n, config)` holds n independent episodes in HBM and
+exposes the reference's reset / step API (env/quadcopter_env.py:111-232) on
+tensors.  Each call is one kernel launch (include/quadtrack.h ABI 9):
+
+  reset(seeds)   qt_seed_draws + qt_frame_reset (numpy default_rng(seed)'s
+                 draws on the device, quadcopter_env.py:111-150)
+  step(actions)  qt_frame_step: action validation, RK4 / Euler, state
+                 constraints, post-step tracking error, reward, termination,
+                 info, for every episode (quadcopter_env.py:152-293)
+  step_closed(controller)
+                 qt_frame_closed_step: the controller's compute_action on the
+                 current observation, then the step, in one launch
+
+Every step writes a new observation frame (quadtrack.step.Frame); the
+returned observation / reward / done / info tensors are views of it.  The
+caller owns them and no later step writes into them, as the reference's
+observation arrays are fresh copies (quadcopter_env.py:481-486).  The next
+step reads its state from the last frame, so writing into the returned
+tensors in place would change the environment: the env detects that (the
+views share one version counter) and raises instead.
 """
 
 from __future__ import annotations
+
+import ctypes as C
 
 import numpy as np
 import torch
 
 from .. import _abi, core
-from .._abi import ACC_ON_POST, ACC_STEPS, ACC_VIOLATIONS, MOTIONS
+from .._abi import FB_DONE, FR_X, MOTIONS, check, raw_stream
+from ..step import Frame, action_tensor
 from . import seeding
 from .config import as_env_config
 
@@ -50,39 +65,66 @@ def motion_indices(motion, n: int) -> np.ndarray:
 
 
 class BatchedQuadcopterEnv:
+    """n QuadcopterEnv episodes stepped together.
+
+    motion      per-episode motion types (names or enum indices; default the config's)
+    mass        per-episode plant mass (default the config's)
+    freeze_done True (default): an episode that is done is not stepped again,
+                its observation and info stay those of its last step (the
+                Evaluator stops stepping at done, eval.py:119-165); False:
+                every episode is stepped on every call, as the reference's
+                env steps after done.
+    """
+
     STATE_DIM = 12
     ACTION_DIM = 4
 
-    def __init__(self, num_envs: int, config=None, device=None, motion=None, mass=None):
-        if num_envs < 1:
-            raise ValueError("num_envs must be >= 1")
+    def __init__(self, num_envs: int, config=None, device=None, motion=None, mass=None, freeze_done: bool = True):
+        if num_envs < 0:
+            raise ValueError("num_envs must be >= 0")
         self.config = as_env_config(config)
         self.params = self.config.to_params()
         self.num_envs = int(num_envs)
         self.device = _abi.require_gpu(device)
+        self.freeze_done = bool(freeze_done)
         n, dev = self.num_envs, self.device
         self.motion = None
         if motion is not None:
             self.motion = torch.as_tensor(motion_indices(motion, n), device=dev)
         self.plant_mass = None if mass is None else core.to_device(np.broadcast_to(np.asarray(mass, float), (n,)), dev)
-        self.state = core.RolloutState.empty(n, dev)
-        self.batch: core.EpisodeBatch | None = None
-        self._dummy_K = torch.zeros(24, 1, dtype=F64, device=dev)
+        self.pattern: torch.Tensor | None = None
+        self.offset: torch.Tensor | None = None
+        self._frame: Frame | None = None
+        self._env_ref = C.byref(self.params)
+        self._batch = None
+        self._closed = None  # (controller, its qt_batch, byref) of step_closed
 
     # ---------------------------------------------------------------- reset
     def reset_from_draws(self, pattern, offset):
         """Reset every episode from explicit draws: pattern [4, n], offset [3, n]."""
         n, dev = self.num_envs, self.device
-        self.batch = core.EpisodeBatch(n=n, device=dev, pattern=core.to_device(pattern, dev),
-                                       offset=core.to_device(offset, dev), K=self._dummy_K, k_cols=6,
-                                       motion=self.motion, plant_mass=self.plant_mass)
-        core.validate(self.batch, self.state)
-        core.reset(self.params, self.batch, self.state)
-        return self.observation()
+        self.pattern = core.to_device(pattern, dev)
+        self.offset = core.to_device(offset, dev)
+        core._check_cols("pattern", self.pattern, 4, n)
+        core._check_cols("offset", self.offset, 3, n)
+        b = _abi.Batch()
+        b.n = n
+        b.motion = None if self.motion is None else self.motion.data_ptr()
+        b.pattern = self.pattern.data_ptr()
+        b.plant_mass = None if self.plant_mass is None else self.plant_mass.data_ptr()
+        self._batch = b
+        self._batch_ref = C.byref(b)
+        self._closed = None
+        fr = Frame(n, dev)
+        with torch.cuda.device(dev):
+            check(_abi.load().qt_frame_reset(self._env_ref, self._batch_ref, self.offset.data_ptr(), fr.ptr,
+                                             raw_stream(dev)), "qt_frame_reset")
+        self._frame = fr.seal()
+        return fr.observation()
 
     def reset(self, seeds=None):
         """QuadcopterEnv.reset(seed) for every episode: seeds [n] (default
-        config.seed + arange(n))."""
+        config.seed + arange(n)).  Returns the observation dict ([n, 3] tensors)."""
         if seeds is None:
             seeds = self.config.seed + np.arange(self.num_envs)
         seeds = np.asarray(seeds.cpu() if isinstance(seeds, torch.Tensor) else seeds, dtype=np.int64).reshape(-1)
@@ -93,53 +135,92 @@ class BatchedQuadcopterEnv:
         return self.reset_from_draws(pat, off)
 
     # ----------------------------------------------------------------- step
-    def step(self, actions):
-        """actions [n, 4] (thrust, roll, pitch, yaw rates) -> (obs, reward [n],
-        done [n] bool, info dict of tensors)."""
-        if self.batch is None:
+    def _current(self) -> Frame:
+        fr = self._frame
+        if fr is None:
             raise RuntimeError("Environment not initialized. Call reset() first.")
-        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(np.asarray(actions, dtype=np.float64))
-        if a.dim() != 2 or a.shape != (self.num_envs, 4):
-            raise ValueError(f"Action array must have shape ({self.num_envs}, 4), got {tuple(a.shape)}")
-        a = a.to(device=self.device, dtype=F64).T.contiguous()
-        err, on, done, term, viol = core.env_step(self.params, self.batch, a, self.state)
-        acc = self.state.acc
-        steps = acc[ACC_STEPS]
-        info = {
-            "time": self.state.t.clone(),
-            "step": steps.to(torch.int64),
-            "tracking_error": err,
-            "on_target": on,
-            "on_target_ratio": torch.where(steps > 0, acc[ACC_ON_POST] / steps.clamp(min=1), torch.zeros_like(steps)),
-            "action_violations": acc[ACC_VIOLATIONS].to(torch.int64),
-            "termination_code": term,
-            "violation": viol,
-        }
-        return self.observation(), -err, done, info
+        fr.check_intact()
+        return fr
+
+    def step(self, actions):
+        """actions [n, 4] (thrust, roll, pitch, yaw rates; any strides, e.g. a
+        controller's output) or a dict of [n] tensors -> (obs, reward [n],
+        done [n] bool, info dict of [n] tensors)."""
+        fr = self._current()
+        n, dev = self.num_envs, self.device
+        a = action_tensor(actions, n, dev)
+        out = Frame(n, dev)
+        with torch.cuda.device(dev):
+            check(_abi.load().qt_frame_step(self._env_ref, self._batch_ref, fr.ptr,
+                                            _abi.View(a.data_ptr(), a.stride(1), a.stride(0)), out.ptr,
+                                            int(self.freeze_done), raw_stream(dev)), "qt_frame_step")
+        self._frame = out.seal()
+        return out.step_result()
+
+    def step_closed(self, controller):
+        """One closed-loop step in ONE launch: `controller.compute_action` on
+        the current observation, then `step` with its command
+        (qt_frame_closed_step).  Same results as
+        `env.step(controller.compute_action(obs))`; info["action"] holds the
+        command ([n, 4]).  With freeze_done, a done episode's controller state
+        is not advanced."""
+        fr = self._current()
+        n, dev = self.num_envs, self.device
+        cb = self._closed_batch(controller)
+        integ = controller._state_for(n)
+        act = torch.empty(4, n, dtype=F64, device=dev)
+        out = Frame(n, dev)
+        with torch.cuda.device(dev):
+            check(_abi.load().qt_frame_closed_step(
+                self._env_ref, controller._ctrl_ref, cb, fr.ptr, None if integ is None else integ.data_ptr(),
+                out.ptr, act.data_ptr(), int(self.freeze_done), raw_stream(dev)), "qt_frame_closed_step")
+        self._frame = out.seal()
+        obs, rew, done, info = out.step_result()
+        info["action"] = act.T
+        return obs, rew, done, info
+
+    def _closed_batch(self, controller):
+        """qt_batch of the env's episodes with the controller's gains (cached)."""
+        controller.c_batch(self.num_envs)
+        key = (controller, controller._cb)
+        if self._closed is None or self._closed[0] != key:
+            b = _abi.Batch()
+            C.memmove(C.addressof(b), C.addressof(controller._cb), C.sizeof(b))  # gains, hover, feed-forward
+            b.n = self.num_envs
+            b.motion, b.pattern, b.plant_mass = self._batch.motion, self._batch.pattern, self._batch.plant_mass
+            self._closed = (key, b, C.byref(b))
+        return self._closed[2]
 
     # ---------------------------------------------------------- observation
     def observation(self) -> dict:
-        x, tg = self.state.x, self.state.target
-        return {
-            "quadcopter": {"position": x[0:3].T.clone(), "velocity": x[3:6].T.clone(),
-                           "attitude": x[6:9].T.clone(), "angular_velocity": x[9:12].T.clone()},
-            "target": {"position": tg[0:3].T.clone(), "velocity": tg[3:6].T.clone(),
-                       "acceleration": tg[6:9].T.clone()},
-            "time": self.state.t.clone(),
-        }
+        """The current observation (views of the last frame)."""
+        return self._current().observation()
+
+    @property
+    def done(self) -> torch.Tensor:
+        return self._current().b[FB_DONE].view(torch.bool)
 
     def get_state_vector(self) -> torch.Tensor:
-        return self.state.x.T.clone()
+        return self._current().f[FR_X:FR_X + 12].T.clone()
 
     def set_state_vector(self, x) -> None:
+        """Replace every episode's 12-state (the observation after this call sees it)."""
+        fr = self._current()
         x = torch.as_tensor(x, dtype=F64, device=self.device)
         if x.shape != (self.num_envs, self.STATE_DIM):
             raise ValueError(f"State must have shape ({self.num_envs}, {self.STATE_DIM}), got {tuple(x.shape)}")
-        self.state.x.copy_(x.T)
+        out = Frame(self.num_envs, self.device)
+        out.buf.copy_(fr.buf)
+        out.f[FR_X:FR_X + 12].copy_(x.T)
+        self._frame = out.seal()
+
+    @property
+    def frame(self) -> Frame:
+        return self._current()
 
     @property
     def time(self) -> torch.Tensor:
-        return self.state.t.clone()
+        return self._current().f[_abi.FR_TIME].clone()
 
     @property
     def dt(self) -> float:

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--motion", default="linear")
+    ap.add_argument("--cases", nargs="*", default=None, help="only these cases (e.g. exact yaw0)")
+    ap.add_argument("--warmup-s", type=float, default=1.0)
     args = ap.parse_args()
 
     import numpy as np
@@ -57,6 +59,10 @@ def main():
         steps = max_steps_for(env)
         for exact in (False, True):
             for rewards in ((False, True) if integrator == "rk4" else (False,)):
+                name = ("exact" if exact else "yaw0") + ("_euler" if integrator == "euler" else "") + \
+                    ("_rewards" if rewards else "")
+                if args.cases is not None and name not in args.cases:
+                    continue
                 st = core.RolloutState.empty(n, dev)
                 reward = torch.zeros(2, n, dtype=torch.float64, device=dev)
 
@@ -71,7 +77,7 @@ def main():
                         core.rollout(env, ctl.ctrl, crit, batch, st, steps)
 
                 t0 = time.perf_counter()
-                while time.perf_counter() - t0 < 1.0:
+                while time.perf_counter() - t0 < args.warmup_s:
                     one()
                     torch.cuda.synchronize()
                 times = []
@@ -84,8 +90,6 @@ def main():
                     times.append(e0.elapsed_time(e1))
                 ms = float(np.median(times))
                 done = float(st.acc[_abi.ACC_STEPS].sum().item())
-                name = ("exact" if exact else "yaw0") + ("_euler" if integrator == "euler" else "") + \
-                    ("_rewards" if rewards else "")
                 print(json.dumps({"case": name, "integrator": integrator, "rewards": rewards, "n": n,
                                   "motion": args.motion, "ms": round(ms, 4), "ms_min": round(min(times), 4),
                                   "env_steps_per_s": round(done / (ms * 1e-3), 1)}), flush=True)

@@ -47,6 +47,11 @@ int main(void) {
   F(qt_ctrl_params, ff_max_acceleration) F(qt_criteria, overshoot_window) F(qt_batch, K) F(qt_batch, k_cols)
   F(qt_batch, order) F(qt_batch, ff) F(qt_state, target)
   printf("QT_ACC_ROWS %d\nQT_MET_ROWS %d\n", QT_ACC_ROWS, QT_MET_ROWS);
+  printf("qt_view %zu\nqt_obs_view %zu\n", sizeof(qt_view), sizeof(qt_obs_view));
+  F(qt_view, rs) F(qt_view, es) F(qt_obs_view, tacc) F(qt_obs_view, time)
+  printf("QT_FR_ROWS %d\nQT_FC_ROWS %d\nQT_FB_ROWS %d\nQT_FR_TIME %d\nQT_FR_RATIO %d\nQT_FB_TERM %d\n",
+         QT_FR_ROWS, QT_FC_ROWS, QT_FB_ROWS, QT_FR_TIME, QT_FR_RATIO, QT_FB_TERM);
+  printf("QT_FRAME_BYTES_1000 %lld\n", (long long)QT_FRAME_BYTES(1000));
   return 0;
 }
 """
@@ -60,15 +65,22 @@ def test_struct_layout_matches_c(tmp_path):
     out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                               check=True).stdout.strip().splitlines())
     cls = {"qt_env_params": _abi.EnvParams, "qt_ctrl_params": _abi.CtrlParams, "qt_criteria": _abi.Criteria,
-           "qt_batch": _abi.Batch, "qt_state": _abi.State}
+           "qt_batch": _abi.Batch, "qt_state": _abi.State, "qt_view": _abi.View, "qt_obs_view": _abi.ObsView}
     for k, v in out.items():
         if k in cls:
             assert C.sizeof(cls[k]) == int(v), k
+        elif k.startswith("QT_"):
+            continue
         elif "." in k:
             s, f = k.split(".")
             assert getattr(cls[s], f).offset == int(v), k
     assert int(out["QT_ACC_ROWS"]) == _abi.ACC_ROWS
     assert int(out["QT_MET_ROWS"]) == _abi.MET_ROWS
+    assert (int(out["QT_FR_ROWS"]), int(out["QT_FC_ROWS"]), int(out["QT_FB_ROWS"])) == \
+        (_abi.FR_ROWS, _abi.FC_ROWS, _abi.FB_ROWS)
+    assert (int(out["QT_FR_TIME"]), int(out["QT_FR_RATIO"]), int(out["QT_FB_TERM"])) == \
+        (_abi.FR_TIME, _abi.FR_RATIO, _abi.FB_TERM)
+    assert int(out["QT_FRAME_BYTES_1000"]) == _abi.frame_bytes(1000)
 
 
 def test_no_gpu_means_loud_failure():

@@ -1,0 +1,76 @@
+"""Host-side checks of the per-step API's frame layout (quadtrack.step,
+include/quadtrack.h qt_frame_row): the views the Python side hands out sit
+exactly where the kernels write (QT_FRAME_BYTES), no GPU needed."""
+
+import numpy as np
+import pytest
+import torch
+
+from quadtrack import _abi
+from quadtrack.step import Frame, action_tensor, frame_words, obs_view_of
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 64, 1001])
+def test_frame_views_follow_the_c_layout(n):
+    fr = Frame(n, torch.device("cpu"))
+    assert fr.buf.numel() * 8 >= _abi.frame_bytes(n) and frame_words(n) * 8 - _abi.frame_bytes(n) < 8
+    base = fr.buf.data_ptr()
+    if n == 0:
+        return
+    # f rows, then the int64 counters, then the int8 flags (QT_FRAME_BYTES order)
+    assert fr.f.data_ptr() == base and fr.f.shape == (_abi.FR_ROWS, n)
+    assert fr.c.data_ptr() == base + _abi.FR_ROWS * n * 8 and fr.c.dtype == torch.int64
+    assert fr.b.data_ptr() == base + (_abi.FR_ROWS + _abi.FC_ROWS) * n * 8 and fr.b.dtype == torch.int8
+    # write through raw row offsets, read through the observation / info views
+    raw = fr.buf.numpy().view(np.uint8)
+    f = raw[:_abi.FR_ROWS * n * 8].view(np.float64).reshape(_abi.FR_ROWS, n)
+    f[:] = np.arange(_abi.FR_ROWS * n, dtype=float).reshape(_abi.FR_ROWS, n)
+    c = raw[_abi.FR_ROWS * n * 8:(_abi.FR_ROWS + _abi.FC_ROWS) * n * 8].view(np.int64).reshape(_abi.FC_ROWS, n)
+    c[:] = np.arange(_abi.FC_ROWS * n).reshape(_abi.FC_ROWS, n)
+    b = raw[(_abi.FR_ROWS + _abi.FC_ROWS) * n * 8:_abi.frame_bytes(n)].reshape(_abi.FB_ROWS, n)
+    b[:] = 0
+    b[_abi.FB_DONE, ::2] = 1
+    b[_abi.FB_TERM] = 3
+    obs, rew, done, info = fr.step_result()
+    np.testing.assert_array_equal(obs["quadcopter"]["position"].numpy(), f[0:3].T)
+    np.testing.assert_array_equal(obs["quadcopter"]["angular_velocity"].numpy(), f[9:12].T)
+    np.testing.assert_array_equal(obs["target"]["acceleration"].numpy(), f[18:21].T)
+    np.testing.assert_array_equal(obs["time"].numpy(), f[_abi.FR_TIME])
+    np.testing.assert_array_equal(rew.numpy(), f[_abi.FR_REWARD])
+    np.testing.assert_array_equal(info["on_target_ratio"].numpy(), f[_abi.FR_RATIO])
+    np.testing.assert_array_equal(info["step"].numpy(), c[_abi.FC_STEP])
+    np.testing.assert_array_equal(info["action_violations"].numpy(), c[_abi.FC_VIOLATIONS])
+    np.testing.assert_array_equal(done.numpy(), np.arange(n) % 2 == 0)
+    assert np.all(info["termination_code"].numpy() == 3)
+    # the frame's own qt_obs_view names the same rows as the generic one
+    v = fr.obs_view()
+    g, _ = obs_view_of(obs, n, torch.device("cpu"), True)
+    for k in ("pos", "vel", "tpos", "tvel", "tacc", "time"):
+        a, bb = getattr(v, k), getattr(g, k)
+        assert (a.p, a.es) == (bb.p, bb.es), k
+        if k != "time":
+            assert a.rs == bb.rs, k
+    assert fr.views_of(obs)
+    obs2 = dict(obs)
+    obs2["quadcopter"] = dict(obs["quadcopter"], position=obs["quadcopter"]["position"].clone())
+    assert not fr.views_of(obs2)
+
+
+def test_in_place_change_of_an_observation_is_detected():
+    fr = Frame(5, torch.device("cpu")).seal()
+    obs = fr.observation()
+    fr.check_intact()
+    obs["target"]["velocity"].mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        fr.check_intact()
+
+
+def test_action_tensor_forms():
+    dev = torch.device("cpu")
+    a = torch.arange(12, dtype=torch.float64).view(4, 3).T  # [3, 4] transpose view
+    assert action_tensor(a, 3, dev) is a
+    d = action_tensor({"thrust": [1.0, 2.0, 3.0], "yaw_rate": torch.ones(3, dtype=torch.float64)}, 3, dev)
+    np.testing.assert_array_equal(d.numpy(), [[1, 0, 0, 1], [2, 0, 0, 1], [3, 0, 0, 1]])
+    np.testing.assert_array_equal(action_tensor(np.ones((3, 4)), 3, dev).numpy(), np.ones((3, 4)))
+    with pytest.raises(ValueError, match="shape"):
+        action_tensor(np.ones((3, 3)), 3, dev)
