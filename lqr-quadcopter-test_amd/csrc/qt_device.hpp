@@ -45,6 +45,12 @@ __device__ __forceinline__ bool same_sign(double a, double b) {
   return sa == sb;
 }
 
+// A rare per-lane case handled in a wave-uniform branch: the common case is
+// computed branch-free for every lane, and only a wavefront holding a lane
+// that needs the rare path enters it (one ballot and a not-taken scalar
+// branch otherwise).  Each lane's result depends on its own inputs only.
+__device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 // ---------------------------------------------------------------- target
 
 // Per-episode constants of a motion pattern, precomputed once per launch.
@@ -350,21 +356,31 @@ template <bool SMALL = false, bool YAW0 = false>
 __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t,
                                            const RateCoef& rk = RateCoef{}) {
   constexpr int NA = YAW0 ? 2 : 3;
-  const double dm = SMALL ? 0.0 : fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
-  if (SMALL || dm <= kSmallAngle) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      double sd, cd;
-      if (YAW0)
-        rate_sincos(delta[i], &sd, &cd, rk);
-      else
-        small_sincos(delta[i], &sd, &cd);
-      t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
-      t.c[i] = fma(t0.c[i], cd, -(t0.s[i] * sd));
+  for (int i = 0; i < NA; ++i) {
+    double sd, cd;
+    if (YAW0)
+      rate_sincos(delta[i], &sd, &cd, rk);
+    else
+      small_sincos(delta[i], &sd, &cd);
+    t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
+    t.c[i] = fma(t0.c[i], cd, -(t0.s[i] * sd));
+  }
+  if (!SMALL) {
+    // a lane with an offset beyond small_sincos' range evaluates the stage
+    // angles directly (a wave-uniform branch; per lane the same choice as
+    // `dm <= kSmallAngle ? rotated : direct`)
+    const double dm = fmax(fabs(delta[0]), fmax(fabs(delta[1]), fabs(delta[2])));
+    const bool big = !(dm <= kSmallAngle);
+    if (any_lane(big)) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        double sv, cv;
+        fast_sincos(ang[i] + delta[i], &sv, &cv);
+        t.s[i] = big ? sv : t.s[i];
+        t.c[i] = big ? cv : t.c[i];
+      }
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) fast_sincos(ang[i] + delta[i], &t.s[i], &t.c[i]);
   }
   if (YAW0) t.s[2] = 0.0, t.c[2] = 1.0;
 }
@@ -781,44 +797,76 @@ __device__ __forceinline__ bool norm_gt(double s, double r) {
   return sqrt(s) > r;
 }
 
-// `sqrt(s) <= r` likewise (NaN -> false).
+// `sqrt(s) <= r` likewise (NaN -> false), branch-free outside the band.
 __device__ __forceinline__ bool norm_le(double s, double r) {
   const double r2 = r * r;
-  if (s < r2 * (1.0 - 1e-14)) return true;
-  if (s > r2 * (1.0 + 1e-14)) return false;
-  return sqrt(s) <= r;
+  bool le = s < r2 * (1.0 - 1e-14);
+  const bool band = !le && !(s > r2 * (1.0 + 1e-14));  // in the band, or NaN
+  if (any_lane(band)) le = band ? sqrt(s) <= r : le;
+  return le;
+}
+
+// numpy's (a + pi) % (2 pi) - pi of the three attitude angles
+// (quadcopter_env.py:457, _normalize_angle 468-470): for |a + pi| < 4 pi
+// (every angle a constrained step produces) the remainder takes at most one
+// exact correction (Sterbenz), computed by selects as py_mod_2pi does; larger
+// magnitudes and infinities take py_mod_2pi's fmod in a wave-uniform branch.
+__device__ __forceinline__ void wrap_angles(double* ang) {
+  double b[3], m[3];
+  bool big[3], any = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    b[i] = ang[i] + kPi;
+    big[i] = !(fabs(b[i]) < 2.0 * kTwoPi) && b[i] == b[i];
+    any = any | big[i];
+    double m1 = b[i] >= kTwoPi ? b[i] - kTwoPi : b[i];
+    m1 = b[i] <= -kTwoPi ? b[i] + kTwoPi : m1;
+    const double m2 = m1 < 0.0 ? m1 + kTwoPi : m1;
+    m[i] = m1 == 0.0 ? 0.0 : m2;  // numpy returns +0.0 for a zero remainder
+  }
+  if (any_lane(any)) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) m[i] = big[i] ? py_mod_2pi(b[i], kTwoPi) : m[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ang[i] = m[i] - kPi;
 }
 
 // _apply_state_constraints (quadcopter_env.py:428-465).  EXACT_NAN keeps
 // np.clip's NaN propagation for the rate / tilt clips (open-loop step on
 // caller-supplied states); inside the fused rollout the state is finite by
 // construction (finite reset, finite clipped actions, bounded updates).
+// The speed clamp acts on a lane whose squared speed reaches within 1e-14 of
+// the limit (norm_gt decides it exactly): a wave-uniform branch.
 template <bool EXACT_NAN = true>
 __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
   const double s = dot3_blas(x[3], x[4], x[5]);
-  if (norm_gt(s, e.max_velocity)) {
+  const bool near = !(s < e.max_velocity * e.max_velocity * (1.0 - 1e-14));  // or NaN
+  if (any_lane(near)) {
+    const bool clamp = near && norm_gt(s, e.max_velocity);
     const double vm = sqrt(s);
 #pragma unroll
-    for (int i = 3; i < 6; ++i) x[i] = x[i] / vm * e.max_velocity;
+    for (int i = 3; i < 6; ++i) x[i] = clamp ? x[i] / vm * e.max_velocity : x[i];
   }
 #pragma unroll
   for (int i = 9; i < 12; ++i)
     x[i] = EXACT_NAN ? clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity)
                      : clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
-#pragma unroll
-  for (int i = 6; i < 9; ++i) x[i] = py_mod_2pi(x[i] + kPi, kTwoPi) - kPi;
+  wrap_angles(x + 6);
   x[6] = EXACT_NAN ? clipd(x[6], -kMaxTilt, kMaxTilt) : clip_num(x[6], -kMaxTilt, kMaxTilt);
   x[7] = EXACT_NAN ? clipd(x[7], -kMaxTilt, kMaxTilt) : clip_num(x[7], -kMaxTilt, kMaxTilt);
 }
 
 // _parse_and_validate_action (quadcopter_env.py:234-293) on an array action;
 // returns true when any violation was recorded.  A finite 4-sum proves every
-// component finite; otherwise the per-component NaN/Inf zeroing runs.
+// component finite; otherwise (a wave-uniform branch) the per-component
+// NaN/Inf zeroing runs.
 __device__ __forceinline__ bool parse_action(const qt_env_params& e, const double* in, double* a) {
   bool viol = false;
 #pragma unroll
   for (int i = 0; i < 4; ++i) a[i] = in[i];
-  if (!isfinite((in[0] + in[1]) + (in[2] + in[3]))) {
+  const bool nf = !isfinite((in[0] + in[1]) + (in[2] + in[3]));
+  if (any_lane(nf)) {  // for a lane with finite components these are no-ops
     const bool finite = isfinite(in[0]) && isfinite(in[1]) && isfinite(in[2]) && isfinite(in[3]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = isfinite(in[i]) ? in[i] : 0.0;
@@ -837,20 +885,23 @@ __device__ __forceinline__ bool parse_action(const qt_env_params& e, const doubl
   return viol;
 }
 
-// _check_termination (quadcopter_env.py:513-535).  A finite sum of the 12
-// bounded components proves them all finite; a non-finite sum falls back to
-// the element test.
+// _check_termination (quadcopter_env.py:513-535) as selects.  A finite sum of
+// the 12 components proves them all finite; a non-finite sum (a wave-uniform
+// branch) falls back to the element test.
 __device__ __forceinline__ int termination(const qt_env_params& e, double t, const double* x) {
-  if (t >= e.max_episode_time) return QT_TERM_TIME_LIMIT;
-  if (fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position) return QT_TERM_POSITION_BOUNDS;
+  const bool tl = t >= e.max_episode_time;
+  const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
   double sum = 0.0;
 #pragma unroll
   for (int i = 0; i < 12; ++i) sum += x[i];
-  if (isfinite(sum)) return QT_TERM_RUNNING;
-  bool fin = true;
+  bool fin = isfinite(sum);
+  if (any_lane(!fin)) {
+    bool f = true;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) fin = fin && isfinite(x[i]);
-  return fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY;
+    for (int i = 0; i < 12; ++i) f = f && isfinite(x[i]);
+    fin = fin || f;
+  }
+  return tl ? QT_TERM_TIME_LIMIT : (pb ? QT_TERM_POSITION_BOUNDS : (fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY));
 }
 
 // ------------------------------------------------- fast-path preconditions
@@ -1091,11 +1142,14 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
       const double g = em > c.integral_zero_threshold ? c.dt : 0.0;
 #pragma unroll
       for (int i = 0; i < 3; ++i) integ[i] = add_product_rn(integ[i], g, ep[i]);
-    } else if (em > c.integral_zero_threshold) {
+    } else {
+      // the threshold gate and the anti-windup block (riccati_lqr.py:873-895)
+      // as selects; I += dt * e rounded as numpy rounds it
+      const bool gate = em > c.integral_zero_threshold;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const bool block = fabs(integ[i]) >= lim && lim > 0 && same_sign(integ[i], ep[i]);
-        if (!block) integ[i] += c.dt * ep[i];
+        integ[i] = (gate && !block) ? add_product_rn(integ[i], c.dt, ep[i]) : integ[i];
       }
     }
     if (FAST) {
@@ -1151,7 +1205,7 @@ __device__ __forceinline__ bool compute_action(const qt_ctrl_params& c, const Ga
   // structured gains have no yaw row: clip(0, -max_rate, max_rate) = 0 for
   // the max_rate >= 0 that fast_path_ok requires
   u[3] = (KS && FAST) ? 0.0 : clip_num(raw3, -c.max_rate, c.max_rate);
-  if (!FAST && !isfinite((raw0 + raw1) + (raw2 + raw3))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
+  if (!FAST && any_lane(!isfinite((raw0 + raw1) + (raw2 + raw3)))) {  // np.clip keeps NaN (e.g. NaN fallback gains)
     u[0] = raw0 != raw0 ? raw0 : u[0];
     u[1] = raw1 != raw1 ? raw1 : u[1];
     u[2] = raw2 != raw2 ? raw2 : u[2];

@@ -302,8 +302,8 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       a.sum_e2 += err * err;
       if (FAST)  // err and max_e are numbers here (finite state): a plain max
         a.max_e = fmax(a.max_e, err);
-      else if (!(err <= a.max_e) && !(a.max_e != a.max_e))
-        a.max_e = err;  // np.max, NaN-propagating
+      else  // np.max, NaN-propagating
+        a.max_e = (!(err <= a.max_e) && !(a.max_e != a.max_e)) ? err : a.max_e;
       const bool on = err <= R;
       a.on_pre += on;
       a.sum_u += un;
@@ -831,7 +831,9 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // compiled in (the grouped kernel leaves it out: its two-waves-per-SIMD
 // register budget has no room, and its fresh passes take qt_reset and
 // metrics_kernel around the launch).
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true>
+// REC (the exact flavour): the launch may record steps (rec) or keep rewards
+// (lc.reward); without them the exact loop carries neither pointer.
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true, bool REC = true>
 __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                              const BatchDev& b, const qt_state& st, int nsteps,
                                              double* __restrict__ rec, int deferred, const LaunchConst& lc,
@@ -965,8 +967,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     }
   } else {
     if (deferred != kExact && wave_ok) return;
-    run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec, n,
-                                         ep, lc.reward);
+    run_steps<false, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
+                                         REC ? rec : nullptr, n, ep, REC ? lc.reward : nullptr);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
   // feed-forward reads them); the stored observation carries the reference's
@@ -982,7 +984,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   if (FRESH && lc.met) store_metrics(cr, a, t, lc.met, n, ep);  // a fresh pass: the metrics rows (metrics_kernel)
 }
 
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false>
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool REC = true>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
@@ -991,7 +993,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   if (FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch) return;
   const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
   if (slot < 0) return;
-  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
+  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI, true, REC>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
 }
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type

@@ -551,7 +551,12 @@ struct ExactLaunch {
   static void run(int deferred, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                   const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec,
                   const LaunchConst& lc) {
-    rollout_kernel<kExact, MOTION, KC, FF, KS><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec, deferred, lc);
+    if (rec || lc.reward)
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, true><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, rec,
+                                                                                     deferred, lc);
+    else  // no recording, no rewards: the loop without either pointer
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
+                                                                                      nullptr, deferred, lc);
   }
 };
 
