@@ -725,17 +725,31 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
 // constant across the four stages.
 // FAST: RK4 known (integrator == 0) and every stage offset proven small.
 // YAW0 (with FAST): yaw identically zero; x[8] and x[11] are left untouched.
-template <bool FAST = false, bool YAW0 = false>
-__device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
+// CARRY (the exact step of the fused rollout): *carry holds sin / cos of the
+// step-start attitude (instead of evaluating them) and receives the trig of
+// the last stage's attitude, whose offset goes to d4 (carry_attitude_trig
+// turns them into the next step's); Euler's one stage takes d4 = dt w.
+template <bool FAST = false, bool YAW0 = false, bool CARRY = false>
+__device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u,
+                                          Trig* carry = nullptr, double* d4 = nullptr) {
   static_assert(FAST || !YAW0, "YAW0 is a fast-path specialisation");
+  static_assert(!(CARRY && (FAST || YAW0)), "CARRY is the exact step's");
   // state components that evolve (YAW0: all but yaw 8 and yaw rate 11)
   auto live = [](int i) { return !YAW0 || (i != 8 && i != 11); };
   const double dt = e.dt;
   double k[12];
   Trig t0, ts;
-  trig_of<YAW0>(x + 6, t0);
+  if (CARRY)
+    t0 = *carry;
+  else
+    trig_of<YAW0>(x + 6, t0);
   derivatives<YAW0>(e, pl, x, u, t0, k);
   if (!FAST && e.integrator == 1) {
+    if (CARRY) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) d4[i] = dt * k[6 + i];
+      trig_shift(x + 6, t0, d4, *carry);
+    }
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
     return;
@@ -775,11 +789,48 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
 #pragma unroll
   for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = dt * k[6 + i];
   trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
+  if (CARRY) {
+    *carry = ts;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) d4[i] = del[i];
+  }
   derivatives<YAW0>(e, pl, tmp, u, ts, k);
   const double h6 = dt / 6.0;
 #pragma unroll
   for (int i = 0; i < 12; ++i)
     if (live(i)) x[i] = x[i] + h6 * (acc[i] + k[i]);
+}
+
+// The exact step's carried attitude trig: sin / cos of the constrained new
+// attitude a1 from those of the last RK4 stage's (t4, offset d4 from the
+// step-start a0), rotated by the exact difference of the rounded angles,
+// r = (a1 - a0) - d4 (O(dt^3) for an RK4 step, the rounding alone for
+// Euler), with tiny_sincos.  An angle that the wrap or the tilt clamp moved,
+// or whose r exceeds kAdvanceAngle, is evaluated directly (a wave-uniform
+// branch).  The carried values follow sin / cos of the angles the reference
+// evaluates with a drift of a few ulp per step (as the fast step's,
+// attitude_trig_resid); a launch starts from the direct evaluation.
+__device__ __forceinline__ void carry_attitude_trig(const double* a0, const double* a1, const double* d4,
+                                                    const Trig& t4, Trig& ta) {
+  bool far[3], any = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double r = (a1[i] - a0[i]) - d4[i];
+    far[i] = !(fabs(r) <= kAdvanceAngle);
+    any = any | far[i];
+    double sd, cm;
+    tiny_sincos(r, &sd, &cm);
+    rotate_cm(t4.s[i], t4.c[i], sd, cm, &ta.s[i], &ta.c[i]);
+  }
+  if (any_lane(any)) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double sv, cv;
+      fast_sincos(a1[i], &sv, &cv);
+      ta.s[i] = far[i] ? sv : ta.s[i];
+      ta.c[i] = far[i] ? cv : ta.c[i];
+    }
+  }
 }
 
 // Clip of a value known to be a number: one v_max + one v_min.  (IEEE maxNum

@@ -41,9 +41,10 @@ def _tuner_stream(lo, hi):
     return out[lo:]
 
 
-def _oracle_shard(config, lo, hi):
-    """(met[n,14], xf[n,12]) of episodes lo..hi-1 of `config` by the oracle."""
-    idx = np.arange(lo, hi)
+def _oracle_shard(config, lo, hi, idx=None):
+    """(met[n,14], xf[n,12]) of episodes lo..hi-1 (or the global indices idx)
+    of `config` by the oracle."""
+    idx = np.arange(lo, hi) if idx is None else np.asarray(idx)
     n = len(idx)
     motion = {3: 3, 4: 2}.get(config)
     motions = idx % 5 if config == 5 else np.full(n, motion)
@@ -92,6 +93,40 @@ def test_workload_sample_vs_oracle(qt, config, lo, n):
         np.testing.assert_array_equal(sh.plant_mass.cpu().numpy(), mass)  # device draws == numpy, bit for bit
     np.testing.assert_allclose(met.T, om, rtol=1e-8, atol=TOL)
     np.testing.assert_allclose(res.state.x.cpu().numpy().T, oxf, rtol=1e-8, atol=TOL)
+
+
+def test_config3_full_size(qt):
+    """Config 3 (BASELINE configs[2]) at its full 65,536 episodes in one
+    launch: LQI with the reference's weights on the sinusoidal target, which
+    diverges (the integral saturates, z falls by hundreds of
+    metres; riccati_lqr.py:870-900).  Size-independent properties on every
+    episode, a seeded 512-episode sample against the oracle, and two of four
+    shards bitwise equal to the full run."""
+    from quadtrack import workloads
+    from quadtrack._abi import MET
+    from quadtrack.rollout import run_closed_loop
+
+    total = workloads.EPISODES[3]
+    full = workloads.build(3)
+    res = run_closed_loop(full.controller, **full.run_kwargs())
+    met = res.metrics.cpu().numpy()
+    steps, term = met[MET["steps"]], met[MET["termination_code"]]
+    assert np.all(np.isfinite(met)) and bool(torch.isfinite(res.state.x).all())
+    # every episode ends: the 3,000-step time limit or the 1,000 m position bound
+    assert np.all((term == 1) & (steps == 3000) | (term == 2) & (steps < 3000))
+    rms, mean, mx = met[MET["rms_tracking_error"]], met[MET["mean_tracking_error"]], met[MET["max_tracking_error"]]
+    assert np.all(rms >= mean - 1e-12) and np.all(mx >= rms - 1e-12)
+    assert np.all(np.abs(res.state.integ[:3].cpu().numpy()) <= 10.0)  # integral_limit
+    assert float(np.median(mean)) > 10.0  # the reference's divergence (SURVEY F7), not a tracking run
+    sample = np.sort(np.random.default_rng(3).choice(total, 512, replace=False))
+    om, oxf, _ = _oracle_shard(3, 0, 0, idx=sample)
+    np.testing.assert_allclose(met[:, sample].T, om, rtol=1e-8, atol=TOL)
+    np.testing.assert_allclose(res.state.x.cpu().numpy()[:, sample].T, oxf, rtol=1e-8, atol=TOL)
+    for r in (1, 2):
+        lo, hi = workloads.shard_bounds(total, r, 4)
+        sh = workloads.build(3, lo, hi)
+        part = run_closed_loop(sh.controller, **sh.run_kwargs())
+        assert torch.equal(part.metrics, res.metrics[:, lo:hi])
 
 
 @pytest.mark.parametrize("config", [4, 5])
