@@ -721,6 +721,69 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
   x[10] = fma(R.wy, w1, R.wu * u[2]);
 }
 
+// One RK4 / Euler step of the exact flavour in closed form, for any attitude
+// and body rates (yaw included): integrate_yaw0's linear maps (RateLin:
+// rates / attitudes, VelLin: velocities / positions; they hold for any w and
+// u, the rate dynamics being linear) with the thrust direction R3 at the
+// four stage attitudes (derivatives: cpsi sth cphi + spsi sphi,
+// spsi sth cphi - cpsi sphi, cth cphi).  The stage trig is the step-start
+// trig `ta` shifted by each stage's offset (trig_shift: small_sincos, or the
+// direct evaluation for an offset beyond its range).  Equal to the staged
+// RK4 up to the rounding of the reassociation (~1e-16 relative per step), as
+// the yaw-at-rest step.  Out: the fourth stage's offsets d4 and trig t4
+// (carry_attitude_trig).  Euler (make_rate_lin / make_vel_lin's one-stage
+// coefficients): stages 2 and 3 carry zero weight and are skipped.
+__device__ __forceinline__ void integrate_closed(const qt_env_params& e, const RateLin& R, const VelLin& L,
+                                                 const Plant& pl, const Trig& ta, double* x, const double* u,
+                                                 double* d4, Trig& t4) {
+  const double w[3] = {x[9], x[10], x[11]};
+  double d2[3], d3[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    d2[i] = R.h2 * w[i];
+    d3[i] = fma(R.d3y, w[i], R.d3u * u[1 + i]);
+    d4[i] = fma(R.d4y, w[i], R.d4u * u[1 + i]);
+  }
+  Trig t[4];
+  t[0] = ta;
+  trig_shift(x + 6, ta, d4, t[3]);
+  t4 = t[3];
+  double sv[3] = {0.0, 0.0, 0.0}, sp[3] = {0.0, 0.0, 0.0};
+  auto add_stage = [&](const Trig& q, double wv, double pa, bool pos) {
+    const double sphi = q.s[0], cphi = q.c[0], sth = q.s[1], cth = q.c[1], spsi = q.s[2], cpsi = q.c[2];
+    const double sc = sth * cphi;
+    const double r0 = fma(cpsi, sc, spsi * sphi), r1 = fma(spsi, sc, -(cpsi * sphi)), r2 = cth * cphi;
+    sv[0] = fma(wv, r0, sv[0]);
+    sv[1] = fma(wv, r1, sv[1]);
+    sv[2] = fma(wv, r2, sv[2]);
+    if (pos) {
+      sp[0] = fma(pa, r0, sp[0]);
+      sp[1] = fma(pa, r1, sp[1]);
+      sp[2] = fma(pa, r2, sp[2]);
+    }
+  };
+  add_stage(t[0], L.wv[0], L.pa[0], true);
+  if (e.integrator != 1) {  // RK4: stages 2 and 3 (uniform)
+    trig_shift(x + 6, ta, d2, t[1]);
+    trig_shift(x + 6, ta, d3, t[2]);
+    add_stage(t[1], L.wv[1], L.pa[1], true);
+    add_stage(t[2], L.wv[2], L.pa[2], true);
+  }
+  add_stage(t[3], L.wv[3], 0.0, false);  // the fourth stage reaches the velocities only (0 for Euler)
+  const double tm = u[0] * pl.inv_mass;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double v = x[3 + j];
+    x[j] = fma(tm, sp[j], fma(L.pv, v, j == 2 ? x[j] + L.gp : x[j]));
+    x[3 + j] = fma(tm, sv[j], j == 2 ? fma(L.cv, v, L.gv) : L.cv * v);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    x[6 + i] = fma(R.ay, w[i], fma(R.au, u[1 + i], x[6 + i]));
+    x[9 + i] = fma(R.wy, w[i], R.wu * u[1 + i]);
+  }
+}
+
 // _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held
 // constant across the four stages.
 // FAST: RK4 known (integrator == 0) and every stage offset proven small.

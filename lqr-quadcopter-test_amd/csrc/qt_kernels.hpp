@@ -273,9 +273,16 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   // last step's tracking error (info["tracking_error"], train.py:630)
   double rew_sum = 0.0, rew_last = 0.0;
   if (!FAST && reward) rew_sum = reward[ep], rew_last = reward[n + ep];
-  // the exact step carries sin / cos of the attitude across steps (carry_attitude_trig)
+  // the exact step: closed-form RK4 / Euler (integrate_closed) with sin / cos
+  // of the attitude carried across steps (carry_attitude_trig)
   Trig ta;
-  if (!FAST) trig_of(x + 6, ta);
+  RateLin rl{};
+  VelLin vl{};
+  if (!FAST) {
+    trig_of(x + 6, ta);
+    rl = make_rate_lin(e);
+    vl = make_vel_lin(e, pl);
+  }
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -348,8 +355,8 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     } else {
       double ua[4], a0[3] = {x[6], x[7], x[8]}, d4[3];
       a.viol += parse_action(e, u, ua);
-      Trig t4 = ta;
-      integrate<false, false, true>(e, pl, x, ua, &t4, d4);
+      Trig t4;
+      integrate_closed(e, rl, vl, pl, ta, x, ua, d4, t4);
       if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
       carry_attitude_trig(a0, x + 6, d4, t4, ta);
       t += e.dt;
