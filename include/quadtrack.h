@@ -319,7 +319,8 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    target's carried rotor once per horizon.  seg_motion must agree with
    batch->motion (when given) for every slot; a wave holding a slot whose
    batch->motion differs is run by the exact pass, which takes each episode's
-   motion from batch->motion. */
+   motion from batch->motion — in the one-launch grouped flavour and in the
+   per-segment launch sets alike. */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);

@@ -884,15 +884,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
       bmul_acc<N>(gr, hr, w);  // W = I + G H
 #pragma unroll
       for (int j = 0; j < N; ++j) w0[j] = w[j];
-      // W^-1 without row exchanges (row_gj_nopiv), checked by the residual of
-      // W (W^-1 1) = 1; a problem that misses it takes row_gj_invert's
-      double myinv = 1.0, srow = 0.0;
+      // W^-1 without row exchanges (row_gj_nopiv), checked by the residuals of
+      // W (W^-1 v) = v for two probes, v = 1 and the alternating v = (1, -1,
+      // 1, ...) (an error of W^-1 that cancels across a row against one probe
+      // shows against the other); a problem that misses either takes
+      // row_gj_invert's
+      double myinv = 1.0, srow = 0.0, salt = 0.0;
       row_gj_nopiv<N>(w, r, myinv);
 #pragma unroll
-      for (int j = 0; j < N; ++j) w[j] *= myinv, srow += w[j];
-      double res = -1.0;
+      for (int j = 0; j < N; ++j) {
+        w[j] *= myinv;
+        srow += w[j];
+        salt += (j & 1) ? -w[j] : w[j];
+      }
+      double res = -1.0, res2 = (r & 1) ? 1.0 : -1.0;  // minus the probes' entry r
       dot_lanes<N>(res, srow, w0);
-      const bool gbad = !group_all<GS>(!(r < N) || fabs(res) <= kInvCheck);
+      dot_lanes<N>(res2, salt, w0);
+      const bool gbad = !group_all<GS>(!(r < N) || (fabs(res) <= kInvCheck && fabs(res2) <= kInvCheck));
       if (QT_DARE_FALLBACK && __ballot(gbad) != 0) {
         int col, pk[N];
         double w2[N];

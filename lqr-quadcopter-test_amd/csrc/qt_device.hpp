@@ -746,7 +746,30 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   }
   Trig t[4];
   t[0] = ta;
-  trig_shift(x + 6, ta, d4, t[3]);
+  trig_shift<true>(x + 6, ta, d4, t[3]);
+  if (e.integrator != 1) {
+    trig_shift<true>(x + 6, ta, d2, t[1]);
+    trig_shift<true>(x + 6, ta, d3, t[2]);
+  }
+  // an offset beyond small_sincos' range: that lane's stage angles are
+  // evaluated directly (one wave-uniform branch for the three stages)
+  double dm = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) dm = fmax(dm, fmax(fabs(d2[i]), fmax(fabs(d3[i]), fabs(d4[i]))));
+  const bool big = !(dm <= kSmallAngle);
+  if (any_lane(big)) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double sv, cv;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const double* d = k == 1 ? d2 : (k == 2 ? d3 : d4);
+        fast_sincos(x[6 + i] + d[i], &sv, &cv);
+        t[k].s[i] = big ? sv : t[k].s[i];
+        t[k].c[i] = big ? cv : t[k].c[i];
+      }
+    }
+  }
   t4 = t[3];
   double sv[3] = {0.0, 0.0, 0.0}, sp[3] = {0.0, 0.0, 0.0};
   auto add_stage = [&](const Trig& q, double wv, double pa, bool pos) {
@@ -764,8 +787,6 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   };
   add_stage(t[0], L.wv[0], L.pa[0], true);
   if (e.integrator != 1) {  // RK4: stages 2 and 3 (uniform)
-    trig_shift(x + 6, ta, d2, t[1]);
-    trig_shift(x + 6, ta, d3, t[2]);
     add_stage(t[1], L.wv[1], L.pa[1], true);
     add_stage(t[2], L.wv[2], L.pa[2], true);
   }
@@ -969,6 +990,59 @@ __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
   wrap_angles(x + 6);
   x[6] = EXACT_NAN ? clipd(x[6], -kMaxTilt, kMaxTilt) : clip_num(x[6], -kMaxTilt, kMaxTilt);
   x[7] = EXACT_NAN ? clipd(x[7], -kMaxTilt, kMaxTilt) : clip_num(x[7], -kMaxTilt, kMaxTilt);
+}
+
+// _apply_state_constraints (quadcopter_env.py:428-465) followed by
+// _check_termination (513-535) at the new time t, with ONE wave-uniform
+// branch for every rare case, its predicates taken on the unconstrained
+// state: the speed clamp (squared speed within 1e-14 of the limit or above;
+// norm_gt decides it), an angle with (a + pi) outside (-2 pi, 4 pi) (numpy's
+// floor-mod by fmod, py_mod_2pi; also NaN), and a non-finite component (the
+// element test, on the constrained state: a clipped infinite rate is finite
+// again).  Otherwise: the rate clip, one exact wrap correction and the tilt
+// clip as selects.  EXACT_NAN: np.clip's NaN propagation in the clips (the
+// per-step API's caller-supplied states); the fused rollout's state is finite.
+template <bool EXACT_NAN = true>
+__device__ __forceinline__ int constrain_terminate(const qt_env_params& e, double* x, double t) {
+  const double s = dot3_blas(x[3], x[4], x[5]);
+  const bool near = !(s < e.max_velocity * e.max_velocity * (1.0 - 1e-14));  // or NaN
+  double sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) sum += x[i];
+  const bool nf = !isfinite(sum);
+  double b[3];
+  bool big[3], rare = near | nf;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    b[i] = x[6 + i] + kPi;
+    big[i] = !(b[i] > -kTwoPi && b[i] < 2.0 * kTwoPi);  // or NaN
+    rare = rare | big[i];
+    // (b % 2 pi) for b in (-2 pi, 4 pi): one exact correction, numpy's rounding
+    const double adj = b[i] < 0.0 ? kTwoPi : (b[i] >= kTwoPi ? -kTwoPi : 0.0);
+    x[6 + i] = (b[i] + adj) - kPi;
+  }
+#pragma unroll
+  for (int i = 9; i < 12; ++i)
+    x[i] = EXACT_NAN ? clipd(x[i], -e.max_angular_velocity, e.max_angular_velocity)
+                     : clip_num(x[i], -e.max_angular_velocity, e.max_angular_velocity);
+  bool fin = true;
+  if (any_lane(rare)) {
+    const bool clamp = near && norm_gt(s, e.max_velocity);
+    const double vm = sqrt(s);
+#pragma unroll
+    for (int i = 3; i < 6; ++i) x[i] = clamp ? x[i] / vm * e.max_velocity : x[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[6 + i] = big[i] ? py_mod_2pi(b[i], kTwoPi) - kPi : x[6 + i];
+    bool f = true;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) f = f && isfinite(x[i]);
+    fin = !nf || f;
+  }
+  x[6] = EXACT_NAN ? clipd(x[6], -kMaxTilt, kMaxTilt) : clip_num(x[6], -kMaxTilt, kMaxTilt);
+  x[7] = EXACT_NAN ? clipd(x[7], -kMaxTilt, kMaxTilt) : clip_num(x[7], -kMaxTilt, kMaxTilt);
+  const bool tl = t >= e.max_episode_time;
+  const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
+  return tl ? QT_TERM_TIME_LIMIT : (pb ? QT_TERM_POSITION_BOUNDS : (fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY));
 }
 
 // _parse_and_validate_action (quadcopter_env.py:234-293) on an array action;

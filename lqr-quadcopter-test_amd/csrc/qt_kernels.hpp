@@ -103,6 +103,11 @@ struct BatchDev {
   int32_t nseg;
   int8_t seg_motion[8];
   int64_t seg_end[8], wave_end[8];
+  // A per-segment launch of a grouped batch (qt_rollout_grouped's one launch
+  // set per group): the group's motion, which its slots' batch->motion must
+  // match (-1: none to check).  A wave holding a slot that does not is left to
+  // the exact pass, which then runs with each episode's own motion.
+  int32_t seg_check;
 };
 
 // The slot a launch position runs, or -1 past the launch's slot range (or in
@@ -243,6 +248,16 @@ __device__ __forceinline__ void overshoot_step(Acc& a, bool on, double over, int
 
 // ---------------------------------------------------------------- rollout
 
+// Sum of squares in the reference's order, ((a^2 + b^2) + c^2) without FMA
+// contraction (np.linalg.norm / the oracle's norm3): with sqrt_pos's
+// correctly rounded root, the fast loop's tracking error equals the exact
+// step's bit for bit on the same state, so its on-target and LQI-gate
+// decisions need no knife-edge band.
+__device__ __forceinline__ double sq3_ref(double a, double b, double c) {
+#pragma clang fp contract(off)
+  return (a * a + b * b) + c * c;
+}
+
 // The closed-loop steps of one lane.  FAST: the branch-light step of
 // qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
 // takes the exact step's decisions; rare lanes/steps (speed at the
@@ -264,6 +279,11 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
     se_pre = ep0 * ep0 + ep1 * ep1 + ep2 * ep2;
   }
+  // exact step: the pre-step tracking error, carried from the previous step's
+  // post-step error (positions are not constrained, so they are the same
+  // number), ||p - p_T|| in np.linalg.norm(axis=1)'s order (sq3_ref)
+  double err_pre = 0.0;
+  if (!FAST) err_pre = sqrt_noscale(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
   // fast steps of a periodic pattern carry its angles' sin / cos (target_state_carried)
   constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
@@ -304,9 +324,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
         err = err_fast;
         un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
       } else {
-        const double ep0 = tg.p[0] - x[0], ep1 = tg.p[1] - x[1], ep2 = tg.p[2] - x[2];
-        err = sqrt(ep0 * ep0 + ep1 * ep1 + ep2 * ep2);
-        un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
+        // sqrt_noscale: correctly rounded (x >= 2^-767), NaN kept; the command is
+        // finite or NaN (clipped), an infinite position has terminated the episode
+        err = err_pre;
+        un = sqrt_noscale(u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3]);
       }
       a.sum_e += err;
       a.sum_e2 += err * err;
@@ -357,21 +378,19 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       a.viol += parse_action(e, u, ua);
       Trig t4;
       integrate_closed(e, rl, vl, pl, ta, x, ua, d4, t4);
-      if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
-      carry_attitude_trig(a0, x + 6, d4, t4, ta);
       t += e.dt;
+      const int term = constrain_terminate<false>(e, x, t);
+      carry_attitude_trig(a0, x + 6, d4, t4, ta);
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
-      a.on_post += norm_le(q0 * q0 + q1 * q1 + q2 * q2, e.target_radius);
+      err_pre = sqrt_noscale(sq3_ref(q0, q1, q2));  // this step's post-step error, the next one's pre-step
+      a.on_post += err_pre <= e.target_radius;
       if (reward) {
         const double pe = sqrt(dot3_blas(q0, q1, q2));  // float(np.linalg.norm(quad_pos - target_pos))
         rew_sum += -pe;
         rew_last = pe;
       }
-      if (QT_ABLATE & QT_ABL_TERMINATION)
-        a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
-      else
-        a.term = termination(e, t, x);
+      a.term = term;
       a.steps += 1;
       if (rec) {
         double* r = rec + (int64_t)s * 16 * n + ep;
@@ -404,15 +423,6 @@ constexpr int kExact = 0, kFast = 1, kYaw0 = 2;
 
 // ------------------------------------------------- yaw-at-rest fast loop
 
-// Sum of squares in the reference's order, ((a^2 + b^2) + c^2) without FMA
-// contraction (np.linalg.norm / the oracle's norm3): with sqrt_pos's
-// correctly rounded root, the fast loop's tracking error equals the exact
-// step's bit for bit on the same state, so its on-target and LQI-gate
-// decisions need no knife-edge band.
-__device__ __forceinline__ double sq3_ref(double a, double b, double c) {
-#pragma clang fp contract(off)
-  return (a * a + b * b) + c * c;
-}
 
 // Carried sin / cos of a periodic target's angles (circular: 1, sinusoidal:
 // 3, figure-8: theta = omega t).  Each step rotates them by the launch's
@@ -928,6 +938,10 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   // inconsistent seg_motion, rollout_grouped_kernel) to this exact pass, which
   // reads the motion per lane
   if (FLAVOR == kExact && b.nseg && b.motion) lane_ok = lane_ok && (int)b.motion[ep] == slot_motion(b, slot);
+  // a per-segment launch (BatchDev::seg_check): a slot whose own motion is not
+  // the segment's fails the wave test in both kernels, so the exact pass (which
+  // then runs with runtime motion, rollout_batch) takes the wave
+  if (b.seg_check >= 0 && b.motion) lane_ok = lane_ok && (int)b.motion[ep] == b.seg_check;
   // structured gains (or any K whose yaw-rate row is zero: qt_batch.k_no_yaw)
   // never command yaw: a yaw at rest stays exactly zero
   // (and, tilt-bounded, roll and pitch inside the tilt clamp: trig_of<YAW0>;
@@ -1058,6 +1072,7 @@ inline BatchDev to_dev(const qt_batch* b) {
   d.hover = b->hover_thrust, d.K = b->K, d.k_cols = b->k_cols, d.k_per_episode = b->k_per_episode;
   d.order = b->order, d.ff = b->ff, d.slot0 = 0, d.slot_end = b->n;
   d.nseg = 0;
+  d.seg_check = -1;
   return d;
 }
 

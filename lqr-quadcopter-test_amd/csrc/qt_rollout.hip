@@ -67,14 +67,13 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(qt_env_params e, Batch
   for (int i = 0; i < 4; ++i) u[i] = action[i * n + ep];
   const bool viol = parse_action(e, u, ua);
   integrate(e, pl, x, ua);
-  constrain(e, x);
   double t = st.t[ep] + e.dt;
+  const int term = constrain_terminate<true>(e, x, t);
   Target tg;
   target_state<true>(e, motion, pt, t, tg);
   const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
   const double err = sqrt(q0 * q0 + q1 * q1 + q2 * q2);
   const bool on = err <= e.target_radius;
-  const int term = termination(e, t, x);
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
 #pragma unroll
@@ -589,10 +588,22 @@ unsigned long long* defer_flag_for(hipStream_t s) {
 
 // run_yaw0's DUAL threshold: kDualBelow, or QT_DUAL_BELOW from the environment
 // (a test knob: 0 turns the clamping no-vote body off, so a test can compare
-// the two loops' results bit for bit)
+// the two loops' results bit for bit; read at each launch so that a test can
+// switch it).  A value that is not a whole number in 0..62 is ignored (the
+// default applies) and reported once on stderr, so a typo cannot silently
+// switch the body off.
 int dual_below() {
-  const char* v = getenv("QT_DUAL_BELOW");
-  return v && *v ? atoi(v) : kDualBelow;
+  const char* s = getenv("QT_DUAL_BELOW");
+  if (!s || !*s) return kDualBelow;
+  char* end = nullptr;
+  const long x = strtol(s, &end, 10);
+  if (*end != '\0' || x < 0 || x > 62) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      fprintf(stderr, "quadtrack: ignoring QT_DUAL_BELOW=%s (not a whole number in 0..62)\n", s);
+    return kDualBelow;
+  }
+  return (int)x;
 }
 
 // The step flavour a launch can take (launch-level preconditions).
@@ -609,10 +620,13 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
 // grouped: b covers a motion-grouped batch in wave-aligned segments and the
 // yaw-at-rest flavour runs it in one launch (rollout_grouped_kernel), the exact
 // pass with runtime motion over the same slot mapping.
+// exact_motion: the exact pass's motion (default `motion`; -1 for a
+// per-segment launch that checks batch->motion, BatchDev::seg_check).
 int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, hipStream_t s, const qt_env_params& e,
                    const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
                    double* rec, bool grouped = false, double* reward = nullptr, const double* fresh_off = nullptr,
-                   double* met = nullptr) {
+                   double* met = nullptr, int exact_motion = -2) {
+  if (exact_motion == -2) exact_motion = motion;
   LaunchConst lc = make_launch_const(e);  // yaw-at-rest closed forms, target rotors
   lc.hz = make_horizon(e, c, lc.rl);       // the yaw-at-rest loop's safe horizon
   lc.hz.dual_below = dual_below();
@@ -630,8 +644,8 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
     lc.fresh_off = nullptr;  // the fast kernel stored the reset state of the waves it left
   }
-  dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, grouped ? -1 : motion, flavor, grid, s, e, c, cr, b, st, nsteps, rec,
-                                lc);
+  dispatch_rollout<ExactLaunch>(kc, ff, ks_eff, grouped ? -1 : exact_motion, flavor, grid, s, e, c, cr, b, st, nsteps,
+                                rec, lc);
   return check_launch();
 }
 
@@ -685,14 +699,29 @@ int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_crit
       return check_launch();
     }
   }
+  // Per-episode motions given: the reset runs on its own with each episode's
+  // motion (a per-segment launch's fresh prologue would form the reset state
+  // of a mislabelled episode with its segment's motion before deferring it),
+  // and the metrics after the last segment.
+  const bool own_reset = fresh_off && batch->motion;
+  if (own_reset) reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(e, b, fresh_off, st);
   for (int32_t i = 0; i < nseg; ++i) {
     b.slot0 = i ? seg_end[i - 1] : 0;
     b.slot_end = seg_end[i];
     if (b.slot_end == b.slot0) continue;
     const int grid = grid_of(b.slot_end - b.slot0);
+    // with per-episode motions given, a slot labelled with another motion than
+    // its segment's goes to the exact pass, which takes each episode's own
+    // motion (seg_check; the same guarantee as the one-launch grouped path)
+    b.seg_check = batch->motion && seg_motion[i] >= 0 ? seg_motion[i] : -1;
     if (launch_rollout(batch->k_cols, ff, ks, no_yaw, seg_motion[i], grid, s, e, c, cr, b, st, nsteps, rec,
-                       false, nullptr, fresh_off, met) != QT_OK)
+                       false, nullptr, own_reset ? nullptr : fresh_off, own_reset ? nullptr : met,
+                       batch->motion ? -1 : seg_motion[i]) != QT_OK)
       return QT_ELAUNCH;
+  }
+  if (own_reset) {
+    metrics_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(cr, batch->n, st.acc, st.t, met);
+    return check_launch();
   }
   return QT_OK;
 }

@@ -74,14 +74,14 @@ __device__ __forceinline__ void env_step_into(const qt_env_params& e, const Batc
   double ua[4];
   const bool viol = parse_action(e, u, ua);
   integrate(e, pl, x, ua);
-  constrain(e, x);  // np.clip's NaN propagation kept: a caller's action may drive the state anywhere
   t += e.dt;
+  // np.clip's NaN propagation kept: a caller's action may drive the state anywhere
+  const int term = constrain_terminate<true>(e, x, t);
   Target tg;
   target_state<true>(e, motion, pt, t, tg);
   const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
   const double err = sqrt(dot3_blas(q0, q1, q2));  // float(np.linalg.norm(quad_pos - target_pos))
   const bool on = err <= e.target_radius;
-  const int term = termination(e, t, x);
   k.step += 1;
   k.viol += viol;
   k.on += on;

@@ -360,17 +360,31 @@ def rollout_rewards(env: EnvParams, ctrl: CtrlParams, crit: Criteria, batch: Epi
 # waves start first and the short ones fill the end of the launch (config 5:
 # 131,072 episodes 4.35 -> 3.93 ms, 1,048,576 23.5 -> 23.1 ms,
 # profiles/r04/grouping_ab.jsonl).  QT_GROUP_ORDER (a comma list of the five
-# motion types) is an A/B knob.
-GROUP_ORDER = tuple(int(v) for v in os.environ.get("QT_GROUP_ORDER", "3,4,2,1,0").split(","))
+# motion types) is an A/B knob, read and validated when a grouping is made.
+DEFAULT_GROUP_ORDER = (3, 4, 2, 1, 0)
+
+
+def group_order() -> tuple:
+    """The motion groups' slot order: QT_GROUP_ORDER if set, else
+    DEFAULT_GROUP_ORDER; a malformed value raises here (not at import)."""
+    raw = os.environ.get("QT_GROUP_ORDER")
+    if raw is None or raw.strip() == "":
+        return DEFAULT_GROUP_ORDER
+    try:
+        order = tuple(int(v) for v in raw.split(","))
+    except ValueError:
+        raise ValueError(f"QT_GROUP_ORDER={raw!r} is not a comma list of the motion types 0..4") from None
+    if sorted(order) != [0, 1, 2, 3, 4]:
+        raise ValueError(f"QT_GROUP_ORDER={raw!r} is not an order of the motion types 0..4")
+    return order
 
 
 def motion_groups(motion):
     """Grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end).
     A device tensor of motion types is grouped on the device (stable sort, one
     5-element read back); a numpy array on the host.  Groups follow
-    GROUP_ORDER; within a group, episodes keep their index order."""
-    if sorted(GROUP_ORDER) != [0, 1, 2, 3, 4]:
-        raise ValueError(f"GROUP_ORDER {GROUP_ORDER} is not an order of the motion types 0..4")
+    group_order(); within a group, episodes keep their index order."""
+    GROUP_ORDER = group_order()
     pos = np.empty(5, np.int64)
     pos[list(GROUP_ORDER)] = np.arange(5)
     if isinstance(motion, torch.Tensor):

@@ -504,36 +504,51 @@ def test_mixed_motion_order_permutation(qt):
     assert b.groups is None
     r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
     g = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
-    assert g.batch.groups is not None and list(g.batch.groups[0]) == list(core.GROUP_ORDER)
+    assert g.batch.groups is not None and list(g.batch.groups[0]) == list(core.group_order())
     assert torch.equal(a.metrics, r.metrics)
     assert torch.equal(a.state.x, r.state.x)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), g.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(a.state.x.cpu().numpy(), g.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
 
 
-def test_grouped_seg_motion_mismatch_runs_exact(qt):
+@pytest.mark.parametrize("case", ["lqr_grouped", "dense_yaw_row_fast", "pid_recorded"])
+def test_grouped_seg_motion_mismatch_runs_exact(qt, case):
     """qt_rollout_grouped with seg_motion labels that disagree with
-    batch.motion (two groups' labels swapped): the grouped kernel leaves those
-    waves to the exact pass, which takes each episode's motion from
-    batch.motion, so the results are still those of the per-lane-motion run."""
+    batch.motion (two groups' labels swapped): the waves holding mislabelled
+    episodes go to the exact pass, which takes each episode's motion from
+    batch.motion, so the results are still those of the per-lane-motion run.
+    In every path: the one-launch grouped yaw-at-rest kernel (Riccati-LQR),
+    per-segment launches of the staged fast flavour (a heuristic-LQR gain
+    with a yaw-rate row) and of the exact step with recording (PID)."""
     import dataclasses
 
-    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.controllers import BatchedLQR, BatchedPID, BatchedRiccatiLQR
     from quadtrack.rollout import build_batch, run_closed_loop
 
     n = 1000
     motion = [i % 5 for i in range(n)]
-    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    record = case == "pid_recorded"
+    if case == "lqr_grouped":
+        ctl = BatchedRiccatiLQR({"dt": 0.01})
+    elif case == "dense_yaw_row_fast":
+        K = BatchedLQR({}).gains()[0].cpu().numpy().copy()
+        K[3, 0], K[3, 4] = 0.02, -0.01  # a yaw-rate row: no yaw-at-rest flavour
+        ctl = BatchedLQR({"K": K})
+    else:
+        ctl = BatchedPID({})
     plain = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion, group_motion=False)
-    a = run_closed_loop(ctl, {}, n=n, batch=plain, max_steps=400)
+    a = run_closed_loop(ctl, {}, n=n, batch=plain, max_steps=400, record=record)
     g = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion)
     sm, se = g.groups
     sm = list(sm)
     sm[1], sm[2] = sm[2], sm[1]
     bad = dataclasses.replace(g, groups=(sm, list(se)))
-    r = run_closed_loop(ctl, {}, n=n, batch=bad, max_steps=400)
+    r = run_closed_loop(ctl, {}, n=n, batch=bad, max_steps=400, record=record)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), r.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(a.state.x.cpu().numpy(), r.state.x.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    if record:
+        np.testing.assert_allclose(np.nan_to_num(a.record.cpu().numpy()), np.nan_to_num(r.record.cpu().numpy()),
+                                   rtol=1e-9, atol=1e-9)
 
 
 def test_grouped_mixed_segment(qt):
@@ -689,13 +704,16 @@ def test_dense_dare_batch_edge_sizes(qt, n, p):
         solve_dare(np.eye(2), np.ones((2, 9)), np.eye(2), np.eye(9))
 
 
+@pytest.mark.parametrize("eps", [0.0, 1e-8, 1e-5])
 @pytest.mark.parametrize("n", [2, 7])
-def test_dense_dare_row_exchange_fallback(qt, n):
-    """A problem whose first doubling matrix W = I + G Q has W[0][0] = 0
-    exactly (G = b b' with b = [1, 2, 0..], Q = c c' + diag(0, 0, 1..) with
-    c = [1, -1, 0..]): the row kernel's inverse without row exchanges breaks
-    down there, its residual check sends the problem to the pivoted
-    inversion, and the result is the DARE's solution.  It shares its
+def test_dense_dare_row_exchange_fallback(qt, n, eps):
+    """A problem whose first doubling matrix W = I + G Q has a leading pivot
+    W[0][0] = eps: exactly 0 (G = b b' with b = [1, 2, 0..],
+    Q = (1 - eps) c c' + diag(0, 0, 1..) with c = [1, -1, 0..]), or tiny but
+    nonzero.  The row kernel's inverse without row exchanges breaks down or
+    loses accuracy there; its residual checks (two probe vectors) either pass
+    an accurate enough inverse or send the problem to the pivoted inversion,
+    and either way the result is the DARE's solution.  It shares its
     wavefront with benign problems, which keep the exchange-free path; every
     problem satisfies its DARE and K = (R + B'PB)^-1 B'PA.  n = 2 and 7 reach
     the 6- and 9-row kernels."""
@@ -707,12 +725,12 @@ def test_dense_dare_row_exchange_fallback(qt, n):
     b0[:2, 0] = [1.0, 2.0]
     c0 = np.zeros(n)
     c0[:2] = [1.0, -1.0]
-    q0 = np.outer(c0, c0) + np.diag([0.0, 0.0] + [1.0] * (n - 2))
+    q0 = (1.0 - eps) * np.outer(c0, c0) + np.diag([0.0, 0.0] + [1.0] * (n - 2))
     A = np.stack([0.5 * np.eye(n) + (0 if i % 2 == 0 else 0.1 * rng.normal(size=(n, n))) for i in range(m)])
     B = np.stack([b0 if i % 2 == 0 else rng.normal(size=(n, p)) for i in range(m)])
     Q = np.stack([q0 if i % 2 == 0 else np.eye(n) for i in range(m)])
     R = np.stack([np.eye(p) for _ in range(m)])
-    assert (np.eye(n) + B[0] @ B[0].T @ Q[0])[0, 0] == 0.0
+    assert abs((np.eye(n) + B[0] @ B[0].T @ Q[0])[0, 0] - eps) <= 1e-15
     dev = torch.device("cuda:0")
 
     def soa(x):

@@ -102,3 +102,56 @@ def test_rewards_fast_flavour_matches_exact(controller, motion):
         np.testing.assert_array_equal(a[_abi.ACC_STEPS], ae[_abi.ACC_STEPS])
         np.testing.assert_array_equal(a[_abi.ACC_ON_POST], ae[_abi.ACC_ON_POST])
         np.testing.assert_allclose(r, re, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["yaw_row_fast", "euler_yaw0"])
+@pytest.mark.parametrize("chunks", [[1200], [401, 555, 244]])
+def test_rewards_other_fast_flavours_match_step_api(variant, chunks):
+    """qt_rollout_rewards on the fast flavours test_rewards_fast_flavour_matches_exact
+    does not reach: the staged fast step (a heuristic-LQR gain with a
+    yaw-rate row, where the reward comes from sqrt_noscale errors and the
+    boundary terms from sqrt_pos) and the Euler closed form of the
+    yaw-at-rest flavour; in one launch and in uneven chunks.  Reference: the
+    same episodes stepped through the per-step API (BatchedQuadcopterEnv.step_closed,
+    its own exact-step kernel), the reward summed per step in order, the last
+    post-step error, the step and on-target counts."""
+    import torch
+
+    from quadtrack import BatchedQuadcopterEnv, _abi, core
+    from quadtrack.controllers import BatchedLQR, BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch
+    from quadtrack.train import env_config_for
+
+    dev = _abi.require_gpu()
+    cfg = env_config_for(7, "circular", 12.0)
+    if variant == "euler_yaw0":
+        cfg.simulation.integrator = "euler"
+        ctl = BatchedRiccatiLQR({"dt": 0.01}, device=dev)
+    else:
+        K = BatchedLQR({}).gains()[0].cpu().numpy().copy()
+        K[3, 0], K[3, 4] = 0.02, -0.01
+        ctl = BatchedLQR({"K": K}, device=dev)
+    env = cfg.to_params()
+    n = 300
+    batch = build_batch(ctl, cfg, n, seeds=np.arange(n))
+    st = core.RolloutState.empty(n, dev)
+    core.reset(env, batch, st)
+    reward = torch.zeros(2, n, dtype=torch.float64, device=dev)
+    for k in chunks:
+        core.rollout_rewards(env, ctl.ctrl, core.criteria(), batch, st, k, reward)
+    # the per-step API over the same episodes (freeze_done: the rollout stops at done)
+    benv = BatchedQuadcopterEnv(n, cfg)
+    benv.reset(np.arange(n))
+    total = torch.zeros(n, dtype=torch.float64, device=dev)
+    last = torch.zeros(n, dtype=torch.float64, device=dev)
+    done_prev = torch.zeros(n, dtype=torch.bool, device=dev)
+    for _ in range(sum(chunks)):
+        _, r, done, info = benv.step_closed(ctl)
+        active = ~done_prev
+        total = torch.where(active, total + r, total)
+        last = torch.where(active, info["tracking_error"], last)
+        done_prev = done.clone()
+    np.testing.assert_array_equal(st.acc[_abi.ACC_STEPS].cpu().numpy(), info["step"].cpu().numpy())
+    np.testing.assert_array_equal(st.acc[_abi.ACC_ON_POST].cpu().numpy(), info["on_target_count"].cpu().numpy())
+    np.testing.assert_allclose(reward[0].cpu().numpy(), total.cpu().numpy(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(reward[1].cpu().numpy(), last.cpu().numpy(), rtol=1e-9, atol=1e-9)

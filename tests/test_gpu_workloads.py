@@ -190,23 +190,35 @@ def test_batched_tuner_vs_sequential_oracle(qt, horizon):
     assert res.best_score == pytest.approx(best, rel=1e-9, abs=1e-9)
 
 
-def test_clamping_no_vote_body_is_bitwise_the_voted_loop(qt, monkeypatch):
+@pytest.mark.parametrize("case", ["circular", "sinusoidal", "figure8", "pid_circular", "pid_figure8"])
+def test_clamping_no_vote_body_is_bitwise_the_voted_loop(qt, monkeypatch, case):
     """run_yaw0's DUAL body (a clamping no-vote horizon for waves whose
     tilt-bounded horizon is short) against the same launches with it turned
     off (QT_DUAL_BELOW=0: those waves take voted steps): every metric and the
-    final state bit for bit, on config-4 waves (tuner candidates, circular),
-    where a lane at the tilt clamp makes 46% of the steps voted without it."""
+    final state bit for bit.  Riccati-LQR on config-4 waves (tuner candidates;
+    on the circular target a lane at the tilt clamp makes 46% of the steps
+    voted without it) for each target DUAL is compiled for, and a saturating
+    PID (the 3-column loop) whose lanes sit at the tilt clamp."""
     from quadtrack import workloads
+    from quadtrack.controllers import BatchedPID
     from quadtrack.rollout import run_closed_loop
 
     sh = workloads.build(4, 100000, 100000 + 2048)
+    kw = sh.run_kwargs()
+    ctl = sh.controller
+    motion = case.split("_")[-1]
+    kw["env_config"] = {"target": {"motion_type": motion, "speed": 3.0 if case.startswith("pid") else 1.0}}
+    if case.startswith("pid"):
+        ctl = BatchedPID({"kp_pos": [2.0, 2.0, 30.0], "kd_pos": [1.0, 1.0, 10.0], "max_thrust": 18.0,
+                          "max_rate": 2.0})
+        kw["n"] = 2048
     res = []
     for below in ("0", None):
         if below is None:
             monkeypatch.delenv("QT_DUAL_BELOW", raising=False)
         else:
             monkeypatch.setenv("QT_DUAL_BELOW", below)
-        r = run_closed_loop(sh.controller, **sh.run_kwargs())
+        r = run_closed_loop(ctl, **kw)
         res.append((r.metrics.clone(), r.state.x.clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])

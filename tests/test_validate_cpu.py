@@ -53,9 +53,36 @@ def test_motion_groups_layout(counts):
     m = np.concatenate([np.full(c, k, np.int8) for k, c in enumerate(counts)])
     m = m[np.random.default_rng(0).permutation(m.size)]
     order, sm, se = core.motion_groups(m)
-    assert sm == [k for k in core.GROUP_ORDER if counts[k]]
+    assert sm == [k for k in core.group_order() if counts[k]]
     assert se[-1] == m.size and sorted(order.tolist()) == list(range(m.size))
     for k, a, b in zip(sm, [0] + se[:-1], se):
         assert np.array_equal(order[a:b], np.nonzero(m == k)[0])
     to, tsm, tse = core.motion_groups(torch.as_tensor(m))
     assert np.array_equal(to.numpy(), order) and tsm == sm and tse == se
+
+
+def test_group_order_knob_is_validated_when_used(monkeypatch):
+    """QT_GROUP_ORDER (an A/B knob) is read when a grouping is made: a
+    malformed value raises there with the variable named, and never breaks
+    the import of quadtrack.core."""
+    import os
+    import subprocess
+    import sys
+
+    import numpy as np
+
+    from conftest import ROOT
+
+    env = dict(os.environ, QT_GROUP_ORDER="3,,4",
+               PYTHONPATH=os.path.join(ROOT, "lqr-quadcopter-test_amd") + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    subprocess.run([sys.executable, "-c", "import quadtrack.core"], env=env, check=True)
+    monkeypatch.setenv("QT_GROUP_ORDER", "3,,4")
+    with pytest.raises(ValueError, match="QT_GROUP_ORDER"):
+        core.motion_groups(np.array([0, 1, 2], dtype=np.int8))
+    monkeypatch.setenv("QT_GROUP_ORDER", "0,1,2,3,3")
+    with pytest.raises(ValueError, match="QT_GROUP_ORDER"):
+        core.group_order()
+    monkeypatch.setenv("QT_GROUP_ORDER", "0,1,2,3,4")
+    assert core.group_order() == (0, 1, 2, 3, 4)
+    monkeypatch.delenv("QT_GROUP_ORDER")
+    assert core.group_order() == core.DEFAULT_GROUP_ORDER
