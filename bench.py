@@ -15,6 +15,11 @@ after it (returns at once when no wave was deferred), then the summary's two
 launches (partials, + one async RCCL all-reduce of the sums when N > 1).
 value = all ranks' env-steps / max-over-ranks wall time.
 
+Beside it (rank 0, N = 1, untimed for `value`): the per-step API leg
+(`step_api`: 1,048,576 episodes stepped one launch per step from Python by
+BatchedQuadcopterEnv.step_closed, the state round-tripping HBM each step;
+GB/s against the 8 TB/s HBM peak), the DARE throughput and the CPU baseline.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 runs one process per GPU under torch.distributed.run: when WORLD_SIZE is
 unset, bench.py starts `python -m torch.distributed.run --nproc-per-node N`
@@ -68,6 +73,9 @@ def parse():
     ap.add_argument("--cpu-sample-1core", type=int, default=4096, help="episodes of the 1-thread CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the OpenMP CPU leg (0: see cpu_baseline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--step-api-episodes", type=int, default=1048576,
+                    help="episodes of the per-step API leg (rank 0, N=1; 0 skips it)")
+    ap.add_argument("--step-api-steps", type=int, default=100)
     ap.add_argument("--profile-dir", default=PROFILE_DIR,
                     help="committed rocprofv3 summaries (kernel_stats.csv, pmc_*.csv) the line cites")
     ap.add_argument("--launcher-check", action="store_true",
@@ -303,6 +311,10 @@ def main():
         dare = {"problems": m, "seconds_incl_host_setup": round(td, 4), "solves_per_s": round(m / td, 1),
                 "max_iterations": int(b.iters.max().item()), "shared_gain_solve_s": round(t_dare, 4)}
 
+    step_api = None
+    if rank == 0 and world == 1 and args.step_api_episodes > 0:
+        step_api = step_api_leg(args, cfg, dev)
+
     cpu = None
     track = {"mean_tracking_error": res_summary.mean_tracking_error,
              "mean_on_target_ratio": res_summary.mean_on_target_ratio}
@@ -379,10 +391,61 @@ def main():
             "cpu_baseline": cpu,
             "tracking": track,
             "dare": dare,
+            "step_api": step_api,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# HBM bytes per env-step the per-step API's closed step must move by its
+# contract (DESIGN.md §4 "Per-step API"): it reads the previous frame's state
+# (12), target position and velocity (6), time (1), the three counters and
+# the done flag, and the linear pattern (3); it writes the new frame
+# (25 doubles, 3 counters, 5 flags) and the action (4 doubles).
+STEP_API_BYTES = (12 + 6 + 1 + 3) * 8 + 1 + 3 * 8 + (25 + 3) * 8 + 5 + 4 * 8
+
+
+def step_api_leg(args, cfg, dev):
+    """The per-step API at --step-api-episodes episodes: --step-api-steps
+    one-launch closed-loop steps (BatchedQuadcopterEnv.step_closed,
+    qt_frame_closed_step) from Python, HIP events on the launch stream around
+    the loop (the loop is GPU-bound at this size: host issue < kernel time).
+    The HBM roofline of the state round-tripping HBM every step:
+    contract bytes / time per step against the 8 TB/s peak; the kernel's own
+    rocprofv3 trace and FETCH / WRITE counters are in profiles/."""
+    import torch
+
+    from quadtrack import BatchedQuadcopterEnv
+    from quadtrack.controllers import BatchedRiccatiLQR
+
+    n, k = args.step_api_episodes, args.step_api_steps
+    ctl = BatchedRiccatiLQR({"dt": 0.01}, device=dev)
+    env = BatchedQuadcopterEnv(n, cfg, device=dev)
+    ctl.reset(n)
+    env.reset(np.arange(n))
+    for _ in range(10):
+        env.step_closed(ctl)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(s)
+    for _ in range(k):
+        env.step_closed(ctl)
+    e1.record(s)
+    host_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / k
+    gbps = STEP_API_BYTES * n / (ms * 1e-3) / 1e9
+    out = {"episodes": n, "steps": k, "launches_per_step": 1, "ms_per_step": round(ms, 5),
+           "env_steps_per_s": round(n / (ms * 1e-3), 1), "host_us_per_step": round(host_s / k * 1e6, 2),
+           "contract_bytes_per_env_step": STEP_API_BYTES, "hbm_GBps": round(gbps, 1),
+           "hbm_frac": round(gbps / HBM_PEAK_GBS, 4),
+           "kernel": "closed_step_kernel<6, no-FF, structured K, freeze> (qt_frame_closed_step)"}
+    del env, ctl
+    torch.cuda.empty_cache()
+    return out
 
 
 def profiled_kernel(profile_dir, tag):

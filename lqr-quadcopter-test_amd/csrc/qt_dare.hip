@@ -868,6 +868,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
   double ar[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) ar[j] = a_in(j);
+  double rel_prev = INFINITY;  // the last doubling's |dH|_F^2 / |H|_F^2
 
   // ---- doublings: W = I + G H ; Winv = W^-1 ; Y1 = Winv A ; Y2 = Winv G ;
   // H += sym(A' H Y1) ; G += sym(A Y2 A') ; A = A Y1, until |dH|_F <= tol |H|_F
@@ -959,8 +960,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
     }
     dn = group_sum<GS>(r < N ? dn : 0.0);
     hn = group_sum<GS>(r < N ? hn : 0.0);
-    // |dH|_F <= tol |H|_F, squared (tol^2 = 1e-28: no square roots)
-    const int flag = !isfinite(hn) ? -1 : (dn <= kTol * kTol * hn ? 1 : 0);
+    // |dH|_F <= tol |H|_F, squared (tol^2 = 1e-28: no square roots); or, in
+    // the doubling's quadratic regime (this change at most 4x the square of
+    // the last one, relative to |H|), a change below 1e-8 |H|: the next
+    // change, the error left in H, is then below ~1e-16 |H| (one doubling
+    // saved; a linearly converging problem, marginal modes with q_int = 0,
+    // never passes the quadratic test and runs to tol)
+    const double rel = dn / hn;
+    const bool quad = rel <= 1e-16 && rel <= 16.0 * rel_prev * rel_prev;
+    rel_prev = rel;
+    const int flag = !isfinite(hn) ? -1 : ((dn <= kTol * kTol * hn || quad) ? 1 : 0);
     // M = A T2 ; G' = G + M (QT_DARE_SYM: + (M + M') / 2)
     if (QT_DARE_SYM) {
       bmul<N>(ar, t2, mm);
