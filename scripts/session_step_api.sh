@@ -4,8 +4,8 @@
 # steps:
 #   tests  pytest of the per-step API (tests/test_gpu_batched_env.py; PYTEST_ARGS adds)
 #   bench  scripts/step_api_bench.py at 65,536 and 1,048,576 episodes, both modes, LQR and LQI
-#   trace  rocprofv3 kernel trace + stats of the bench loop (1,048,576 and 65,536 episodes, 300 steps)
-#   pmc    FETCH_SIZE and WRITE_SIZE passes of the same loop (1,048,576 episodes, 30 steps)
+#   trace  rocprofv3 kernel trace + stats of the bench loop (1,048,576 and 65,536 episodes, 3,000 steps)
+#   pmc    FETCH_SIZE and WRITE_SIZE passes of the same loop (1,048,576 and 65,536 episodes, 300 steps)
 #   exact  the exact step at 65,536 linear LQR episodes (scripts/flavour_timing.py --cases exact):
 #          timing, kernel trace, SQ / SQ2 / F64 passes
 # Outputs under gpurun_out/$TAG/.  The first failing step ends the session.
@@ -29,13 +29,16 @@ for step in ${STEPS:-tests bench}; do
            cat $O/step_api.jsonl ;;
     trace) for n in 1048576 65536; do
              timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$n -o run -- \
-               python3 $LOOP --n $n --steps 300 --warm 20 > $O/trace_$n.log 2>&1 || fail trace $O/trace_$n.log
+               python3 $LOOP --n $n --steps 3000 --warm 20 > $O/trace_$n.log 2>&1 || fail trace $O/trace_$n.log
              cp $(find $O/trace_$n -name "*kernel_stats.csv" | head -1) $O/step_api_kernel_stats_$n.csv
            done ;;
-    pmc) for P in FETCH_SIZE WRITE_SIZE; do
-           timeout -k 10 -s KILL 300 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$P -o run -- \
-             python3 $LOOP --n 1048576 --steps 30 --warm 5 > $O/pmc_$P.log 2>&1 || fail pmc $O/pmc_$P.log
-           python3 scripts/pmc_summary.py $O/step_api_pmc_$P.csv $(find $O/pmc_$P -name "*counter_collection.csv")
+    pmc) for n in 1048576 65536; do
+           for P in FETCH_SIZE WRITE_SIZE; do
+             timeout -k 10 -s KILL 300 rocprofv3 --pmc $P --output-format csv -d $O/pmc_${P}_$n -o run -- \
+               python3 $LOOP --n $n --steps 300 --warm 5 > $O/pmc_${P}_$n.log 2>&1 || fail pmc $O/pmc_${P}_$n.log
+             python3 scripts/pmc_summary.py $O/step_api_pmc_${P}_$n.csv \
+               $(find $O/pmc_${P}_$n -name "*counter_collection.csv")
+           done
          done ;;
     exact) timeout -k 10 300 python -u scripts/flavour_timing.py --cases exact yaw0 > $O/exact_timing.jsonl 2> $O/exact.err \
              || fail exact $O/exact.err
