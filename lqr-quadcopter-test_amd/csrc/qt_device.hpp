@@ -731,7 +731,7 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
 // direct evaluation for an offset beyond its range).  Equal to the staged
 // RK4 up to the rounding of the reassociation (~1e-16 relative per step), as
 // the yaw-at-rest step.  Out: the fourth stage's offsets d4 and trig t4
-// (constrain_terminate's CARRY).  Euler (make_rate_lin / make_vel_lin's one-stage
+// (carry_attitude_trig).  Euler (make_rate_lin / make_vel_lin's one-stage
 // coefficients): stages 2 and 3 carry zero weight and are skipped.
 __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const RateLin& R, const VelLin& L,
                                                  const Plant& pl, const Trig& ta, double* x, const double* u,
@@ -876,6 +876,38 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
     if (live(i)) x[i] = x[i] + h6 * (acc[i] + k[i]);
 }
 
+// The exact step's carried attitude trig: sin / cos of the constrained new
+// attitude a1 from those of the last RK4 stage's (t4, offset d4 from the
+// step-start a0), rotated by the exact difference of the rounded angles,
+// r = (a1 - a0) - d4 (O(dt^3) for an RK4 step, the rounding alone for
+// Euler), with tiny_sincos.  An angle that the wrap or the tilt clamp moved,
+// or whose r exceeds kAdvanceAngle, is evaluated directly (a wave-uniform
+// branch).  The carried values follow sin / cos of the angles the reference
+// evaluates with a drift of a few ulp per step (as the fast step's,
+// attitude_trig_resid); a launch starts from the direct evaluation.
+__device__ __forceinline__ void carry_attitude_trig(const double* a0, const double* a1, const double* d4,
+                                                    const Trig& t4, Trig& ta) {
+  bool far[3], any = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double r = (a1[i] - a0[i]) - d4[i];
+    far[i] = !(fabs(r) <= kAdvanceAngle);
+    any = any | far[i];
+    double sd, cm;
+    tiny_sincos(r, &sd, &cm);
+    rotate_cm(t4.s[i], t4.c[i], sd, cm, &ta.s[i], &ta.c[i]);
+  }
+  if (any_lane(any)) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double sv, cv;
+      fast_sincos(a1[i], &sv, &cv);
+      ta.s[i] = far[i] ? sv : ta.s[i];
+      ta.c[i] = far[i] ? cv : ta.c[i];
+    }
+  }
+}
+
 // Clip of a value known to be a number: one v_max + one v_min.  (IEEE maxNum
 // would turn a NaN into a bound, which np.clip does not; callers use it only
 // where NaN cannot reach or check for it separately.)
@@ -951,15 +983,6 @@ __device__ __forceinline__ void constrain(const qt_env_params& e, double* x) {
   x[7] = EXACT_NAN ? clipd(x[7], -kMaxTilt, kMaxTilt) : clip_num(x[7], -kMaxTilt, kMaxTilt);
 }
 
-// Attitude trig carried across exact steps (run_steps): sin / cos of the
-// step-start attitude `ta` becomes that of the constrained new attitude.
-struct TrigCarry {
-  const double* a0;  // step-start angles
-  const double* d4;  // the fourth RK4 stage's offsets (integrate_closed)
-  const Trig* t4;    // the fourth stage's trig
-  Trig* ta;          // in: step start; out: the new attitude's
-};
-
 // _apply_state_constraints (quadcopter_env.py:428-465) followed by
 // _check_termination (513-535) at the new time t, with ONE wave-uniform
 // branch for every rare case, its predicates taken on the unconstrained
@@ -970,18 +993,8 @@ struct TrigCarry {
 // again).  Otherwise: the rate clip, one exact wrap correction and the tilt
 // clip as selects.  EXACT_NAN: np.clip's NaN propagation in the clips (the
 // per-step API's caller-supplied states); the fused rollout's state is finite.
-// CARRY (the fused exact step): the new attitude's sin / cos from the fourth
-// stage's, rotated by r = ((a_new - a0) - wrap) - d4 (the exact difference of
-// the rounded angles less the stage offset and the 2 pi correction: O(dt^3),
-// tiny_sincos); a tilt-clamped angle takes sin / cos of the clamp, and an
-// angle whose r exceeds kAdvanceAngle (or that the fmod wrap moved) is
-// evaluated directly, in the same rare branch.  The carried values follow
-// sin / cos of the angles the reference evaluates with a drift of a few ulp
-// per step (as the fast step's, attitude_trig_resid); a launch starts from
-// the direct evaluation.
-template <bool EXACT_NAN = true, bool CARRY = false>
-__device__ __forceinline__ int constrain_terminate(const qt_env_params& e, double* x, double t,
-                                                   const TrigCarry& tc = TrigCarry{}) {
+template <bool EXACT_NAN = true>
+__device__ __forceinline__ int constrain_terminate(const qt_env_params& e, double* x, double t) {
   const double s = dot3_blas(x[3], x[4], x[5]);
   const bool near = !(s < e.max_velocity * e.max_velocity * (1.0 - 1e-14));  // or NaN
   double sum = 0.0;
@@ -989,7 +1002,7 @@ __device__ __forceinline__ int constrain_terminate(const qt_env_params& e, doubl
   for (int i = 0; i < 12; ++i) sum += x[i];
   const bool nf = !isfinite(sum);
   double b[3];
-  bool big[3], far[3] = {false, false, false}, rare = near | nf;
+  bool big[3], rare = near | nf;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     b[i] = x[6 + i] + kPi;
@@ -998,14 +1011,6 @@ __device__ __forceinline__ int constrain_terminate(const qt_env_params& e, doubl
     // (b % 2 pi) for b in (-2 pi, 4 pi): one exact correction, numpy's rounding
     const double adj = b[i] < 0.0 ? kTwoPi : (b[i] >= kTwoPi ? -kTwoPi : 0.0);
     x[6 + i] = (b[i] + adj) - kPi;
-    if (CARRY) {
-      const double r = ((x[6 + i] - tc.a0[i]) - adj) - tc.d4[i];
-      far[i] = big[i] || !(fabs(r) <= kAdvanceAngle);
-      rare = rare | far[i];
-      double sd, cm;
-      tiny_sincos(r, &sd, &cm);
-      rotate_cm(tc.t4->s[i], tc.t4->c[i], sd, cm, &tc.ta->s[i], &tc.ta->c[i]);
-    }
   }
 #pragma unroll
   for (int i = 9; i < 12; ++i)
@@ -1016,13 +1021,6 @@ __device__ __forceinline__ int constrain_terminate(const qt_env_params& e, doubl
     for (int i = 0; i < 2; ++i) {
       const double a = x[6 + i];
       x[6 + i] = EXACT_NAN ? clipd(a, -kMaxTilt, kMaxTilt) : clip_num(a, -kMaxTilt, kMaxTilt);
-      if (CARRY) {
-        // sin / cos of the clamp (constants): fast_sincos(+-kMaxTilt)
-        constexpr double sm = 0.8660254037844386, cm = 0.5000000000000001;
-        const bool lo = a < -kMaxTilt, hi = a > kMaxTilt;
-        tc.ta->s[i] = lo ? -sm : (hi ? sm : tc.ta->s[i]);
-        tc.ta->c[i] = (lo || hi) ? cm : tc.ta->c[i];
-      }
     }
   };
   tilt_clip();
@@ -1039,15 +1037,6 @@ __device__ __forceinline__ int constrain_terminate(const qt_env_params& e, doubl
 #pragma unroll
     for (int i = 0; i < 12; ++i) f = f & isfinite(x[i]);
     fin = !nf || f;
-    if (CARRY) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double sv, cv;
-        fast_sincos(x[6 + i], &sv, &cv);
-        tc.ta->s[i] = far[i] ? sv : tc.ta->s[i];
-        tc.ta->c[i] = far[i] ? cv : tc.ta->c[i];
-      }
-    }
   }
   const bool tl = t >= e.max_episode_time;
   const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;

@@ -294,7 +294,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   double rew_sum = 0.0, rew_last = 0.0;
   if (!FAST && reward) rew_sum = reward[ep], rew_last = reward[n + ep];
   // the exact step: closed-form RK4 / Euler (integrate_closed) with sin / cos
-  // of the attitude carried across steps (constrain_terminate<., true>)
+  // of the attitude carried across steps (carry_attitude_trig)
   Trig ta;
   RateLin rl{};
   VelLin vl{};
@@ -379,7 +379,8 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       Trig t4;
       integrate_closed(e, rl, vl, pl, ta, x, ua, d4, t4);
       t += e.dt;
-      const int term = constrain_terminate<false, true>(e, x, t, TrigCarry{a0, d4, &t4, &ta});
+      const int term = constrain_terminate<false>(e, x, t);
+      carry_attitude_trig(a0, x + 6, d4, t4, ta);
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       err_pre = sqrt_noscale(sq3_ref(q0, q1, q2));  // this step's post-step error, the next one's pre-step

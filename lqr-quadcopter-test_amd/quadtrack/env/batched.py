@@ -13,13 +13,15 @@ tensors.  Each call is one kernel launch (include/quadtrack.h ABI 9):
                  qt_frame_closed_step: the controller's compute_action on the
                  current observation, then the step, in one launch
 
-Every step writes a new observation frame (quadtrack.step.Frame); the
-returned observation / reward / done / info tensors are views of it.  The
-caller owns them and no later step writes into them, as the reference's
-observation arrays are fresh copies (quadcopter_env.py:481-486).  The next
-step reads its state from the last frame, so writing into the returned
-tensors in place would change the environment: the env detects that (the
-views share one version counter) and raises instead.
+Every step writes an observation frame (quadtrack.step.Frame); the returned
+observation / reward / done / info tensors are views of it.  No later step
+writes a frame whose tensors the caller still holds (Frame.recyclable), so
+what the caller keeps stays as it was, as the reference's observation arrays
+are fresh copies (quadcopter_env.py:481-486); a loop that drops them cycles
+through a small pool of frames.  The next step reads its state from the last
+frame, so writing into the returned tensors in place would change the
+environment: the env detects that (the views share one version counter) and
+raises instead.
 """
 
 from __future__ import annotations
@@ -31,7 +33,7 @@ import torch
 
 from .. import _abi, core
 from .._abi import FB_DONE, FR_X, MOTIONS, check, raw_stream
-from ..step import Frame, action_tensor
+from ..step import Frame, FramePool, action_tensor
 from . import seeding
 from .config import as_env_config
 
@@ -95,6 +97,7 @@ class BatchedQuadcopterEnv:
         self.pattern: torch.Tensor | None = None
         self.offset: torch.Tensor | None = None
         self._frame: Frame | None = None
+        self._pool = FramePool(self.num_envs, self.device)  # the frames steps write
         self._env_ref = C.byref(self.params)
         self._batch = None
         self._closed = None  # (controller, its qt_batch, byref) of step_closed
@@ -115,7 +118,8 @@ class BatchedQuadcopterEnv:
         self._batch = b
         self._batch_ref = C.byref(b)
         self._closed = None
-        fr = Frame(n, dev)
+        self._frame = None
+        fr = self._next_frame()
         with torch.cuda.device(dev):
             check(_abi.load().qt_frame_reset(self._env_ref, self._batch_ref, self.offset.data_ptr(), fr.ptr,
                                              raw_stream(dev)), "qt_frame_reset")
@@ -135,6 +139,11 @@ class BatchedQuadcopterEnv:
         return self.reset_from_draws(pat, off)
 
     # ----------------------------------------------------------------- step
+    def _next_frame(self) -> Frame:
+        """The frame the next step writes (FramePool.take: never one the caller
+        holds, nor the current one, which the step reads)."""
+        return self._pool.take(self._frame)
+
     def _current(self) -> Frame:
         fr = self._frame
         if fr is None:
@@ -149,7 +158,7 @@ class BatchedQuadcopterEnv:
         fr = self._current()
         n, dev = self.num_envs, self.device
         a = action_tensor(actions, n, dev)
-        out = Frame(n, dev)
+        out = self._next_frame()
         with torch.cuda.device(dev):
             check(_abi.load().qt_frame_step(self._env_ref, self._batch_ref, fr.ptr,
                                             _abi.View(a.data_ptr(), a.stride(1), a.stride(0)), out.ptr,
@@ -168,16 +177,13 @@ class BatchedQuadcopterEnv:
         n, dev = self.num_envs, self.device
         cb = self._closed_batch(controller)
         integ = controller._state_for(n)
-        act = torch.empty(4, n, dtype=F64, device=dev)
-        out = Frame(n, dev)
+        out = self._next_frame()
         with torch.cuda.device(dev):
             check(_abi.load().qt_frame_closed_step(
                 self._env_ref, controller._ctrl_ref, cb, fr.ptr, None if integ is None else integ.data_ptr(),
-                out.ptr, act.data_ptr(), int(self.freeze_done), raw_stream(dev)), "qt_frame_closed_step")
+                out.ptr, out.act.data_ptr(), int(self.freeze_done), raw_stream(dev)), "qt_frame_closed_step")
         self._frame = out.seal()
-        obs, rew, done, info = out.step_result()
-        info["action"] = act.T
-        return obs, rew, done, info
+        return out.step_result(with_action=True)
 
     def _closed_batch(self, controller):
         """qt_batch of the env's episodes with the controller's gains (cached)."""

@@ -10,9 +10,11 @@ launch over the batch, and what it returns is views, not copies.
 * A `Frame` is one step's output (quadtrack.h qt_frame_row): the state, the
   target observation and the info values of every episode in one contiguous
   SoA block.  The observation dict holds [n, 3] views of it (strides (1, n)),
-  the info dict [n] views.  Each step writes a NEW frame (the allocator
-  recycles dropped ones), so an observation the caller keeps never changes,
-  as the reference's fresh-copy arrays do not (quadcopter_env.py:481-486).
+  the info dict [n] views.  A step never writes a frame any of whose
+  tensors the caller still holds (Frame.recyclable), so an observation the
+  caller keeps never changes, as the reference's fresh-copy arrays do not
+  (quadcopter_env.py:481-486); a loop that drops them cycles through two
+  frames whose views are built once.
 * Views, not transposes: `qt_view` passes any [n, k] tensor layout to the
   kernels by its strides, so the controller reads an observation in place
   and the env reads an action in place (an [n, 4] transpose of the
@@ -26,6 +28,7 @@ is one (qt_frame_closed_step).
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 import torch
@@ -49,23 +52,46 @@ class Observation(dict):
     __slots__ = ("frame",)
 
 
+def _storage_uses(t: torch.Tensor) -> int:
+    """Tensors (views included) sharing t's storage, +1 for the temporary."""
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
+
+
+_CAN_RECYCLE = hasattr(torch._C, "_storage_Use_Count")
+
+
 class Frame:
     """One step's observation + info block (qt_frame_row): f [25, n] float64,
-    c [3, n] int64, b [5, n] int8 views of one device allocation."""
+    c [3, n] int64, b [5, n] int8 views of one device allocation, followed
+    by the [4, n] command rows of a closed-loop step (`act`).
 
-    __slots__ = ("n", "buf", "f", "c", "b", "ptr", "version", "_q", "_obs_view")
+    The tensors a step hands out are built once per frame (`_views`).  A
+    frame is `recyclable` — a later step may write it again — only when
+    nothing outside holds any of it: every handed-out view is back to the
+    Python reference count the frame itself holds, and no other tensor
+    (a slice, a reshape) shares its storage.  So a caller that keeps an
+    observation, a reward, an info value or a view derived from one keeps
+    it unchanged, as with a fresh frame; a loop that drops them lets the
+    env cycle through two frames without allocating or building views."""
+
+    __slots__ = ("n", "buf", "f", "c", "b", "act", "ptr", "version", "_q", "_obs_view", "_views", "_refs",
+                 "_uses", "_info")
 
     def __init__(self, n: int, device):
         self.n = n
-        self.buf = torch.empty(frame_words(n), dtype=F64, device=device)
-        f, c, b = self.buf.split([FR_ROWS * n, FC_ROWS * n, frame_words(n) - (FR_ROWS + FC_ROWS) * n])
+        fw = frame_words(n)
+        self.buf = torch.empty(fw + 4 * n, dtype=F64, device=device)
+        f, c, b, a = self.buf.split([FR_ROWS * n, FC_ROWS * n, fw - (FR_ROWS + FC_ROWS) * n, 4 * n])
         self.f = f.view(FR_ROWS, n)
         self.c = c.view(torch.int64).view(FC_ROWS, n)
         self.b = b.view(torch.int8)[:FB_ROWS * n].view(FB_ROWS, n)
+        self.act = a.view(4, n)
         self.ptr = self.buf.data_ptr()
         self.version = None  # buf._version once a kernel has written it (seal)
         self._q = None
         self._obs_view = None
+        self._views = None
+        self._info = None
 
     def seal(self) -> "Frame":
         """Mark the frame as written: a later in-place change of any of its views
@@ -87,7 +113,10 @@ class Frame:
         return self._q
 
     def observation(self) -> Observation:
-        q = self._quantities()
+        if self._views is None:
+            self._build_views()
+            self._snapshot()
+        q = self._q
         obs = Observation(quadcopter={"position": q[0], "velocity": q[1], "attitude": q[2],
                                       "angular_velocity": q[3]},
                           target={"position": q[4], "velocity": q[5], "acceleration": q[6]},
@@ -95,18 +124,43 @@ class Frame:
         obs.frame = self
         return obs
 
-    def step_result(self):
-        """(obs, reward [n], done [n] bool, info) of QuadcopterEnv.step
-        (quadcopter_env.py:152-232).  info holds every key the reference's
-        info has, as [n] tensors; termination_code / success / episode_length
-        are meaningful where done (the reference adds them only then)."""
+    def _build_views(self):
+        q = self._quantities()
         t, err, rew, ratio = self.f[FR_TIME:FR_TIME + 4].unbind(0)
         step, viol, on_count = self.c.unbind(0)
         done, on, violation, success = self.b[:FB_TERM].view(torch.bool).unbind(0)
-        info = {"time": t, "step": step, "tracking_error": err, "on_target": on, "on_target_ratio": ratio,
-                "action_violations": viol, "termination_code": self.b[FB_TERM], "episode_length": t,
-                "success": success, "violation": violation, "on_target_count": on_count}
-        return self.observation(), rew, done, info
+        self._info = (("time", t), ("step", step), ("tracking_error", err), ("on_target", on),
+                      ("on_target_ratio", ratio), ("action_violations", viol), ("termination_code", self.b[FB_TERM]),
+                      ("episode_length", t), ("success", success), ("violation", violation),
+                      ("on_target_count", on_count))
+        # every tensor a step hands out: reward, done, the command, the observation, the info values
+        self._views = (rew, done, self.act.T) + q + tuple(v for _, v in self._info)
+
+    def _counts(self):
+        return [sys.getrefcount(v) for v in self._views]
+
+    def _snapshot(self):
+        # what the frame itself holds (called with no other reference alive)
+        self._refs = self._counts()
+        self._uses = _storage_uses(self.buf)
+
+    def recyclable(self) -> bool:
+        """True when no view of this frame is held outside it (see the class doc)."""
+        return (self._views is not None and _CAN_RECYCLE and _storage_uses(self.buf) == self._uses
+                and self._counts() == self._refs)
+
+    def step_result(self, with_action: bool = False):
+        """(obs, reward [n], done [n] bool, info) of QuadcopterEnv.step
+        (quadcopter_env.py:152-232).  info holds every key the reference's
+        info has, as [n] tensors; termination_code / success / episode_length
+        are meaningful where done (the reference adds them only then).
+        with_action: info["action"] is the [n, 4] command of a closed-loop step."""
+        obs = self.observation()
+        v = self._views
+        info = dict(self._info)
+        if with_action:
+            info["action"] = v[2]
+        return obs, v[0], v[1], info
 
     def obs_view(self) -> ObsView:
         """The qt_obs_view of this frame's observation (built once)."""
@@ -128,6 +182,30 @@ class Frame:
                     and ot["velocity"] is q[5] and ot.get("acceleration") is q[6] and obs.get("time") is q[7])
         except (KeyError, TypeError):
             return False
+
+
+class FramePool:
+    """The frames an env's steps write (BatchedQuadcopterEnv): `take(cur)`
+    returns a frame that nothing outside the pool holds — neither the Frame
+    object (e.g. `env.frame`, `obs.frame`) nor any tensor it handed out
+    (Frame.recyclable) — other than `cur`, the frame the step reads; else a
+    new one.  The pool keeps `size` frames and forgets the oldest held one
+    past that (its holder owns it)."""
+
+    def __init__(self, n: int, device, size: int = 3):
+        self.n, self.device, self.size = n, device, size
+        self.frames: list[Frame] = []
+
+    def take(self, cur: Frame | None) -> Frame:
+        for fr in self.frames:
+            # references to fr here: the list, the loop variable, getrefcount's argument
+            if fr is not cur and sys.getrefcount(fr) == 3 and fr.recyclable():
+                return fr
+        fr = Frame(self.n, self.device)
+        if len(self.frames) >= self.size:
+            self.frames.remove(next(f for f in self.frames if f is not cur))
+        self.frames.append(fr)
+        return fr
 
 
 def tensor_view(t: torch.Tensor, rows: int, n: int, name: str, device) -> View:

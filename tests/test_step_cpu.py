@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from quadtrack import _abi
-from quadtrack.step import Frame, action_tensor, frame_words, obs_view_of
+from quadtrack.step import Frame, FramePool, action_tensor, frame_words, obs_view_of
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 64, 1001])
@@ -63,6 +63,57 @@ def test_in_place_change_of_an_observation_is_detected():
     obs["target"]["velocity"].mul_(2.0)
     with pytest.raises(RuntimeError, match="modified in place"):
         fr.check_intact()
+
+
+def test_frame_recyclable_only_when_nothing_is_held():
+    """Frame.recyclable (the env's frame pool): true once every tensor a step
+    handed out is dropped, false while the caller holds any of them, a dict
+    holding them, or a view derived from one."""
+    fr = Frame(6, torch.device("cpu")).seal()
+    assert not fr.recyclable()  # never handed out: its views are not built yet
+    assert fr.act.data_ptr() == fr.buf.data_ptr() + frame_words(6) * 8 and fr.act.shape == (4, 6)
+
+    def hold(pick):
+        r = fr.step_result(with_action=True)
+        return pick(*r)
+
+    hold(lambda o, r, d, i: None)
+    assert fr.recyclable() is True
+    for pick in (lambda o, r, d, i: o, lambda o, r, d, i: r, lambda o, r, d, i: d, lambda o, r, d, i: i,
+                 lambda o, r, d, i: o["target"], lambda o, r, d, i: o["time"], lambda o, r, d, i: i["action"],
+                 lambda o, r, d, i: i["termination_code"], lambda o, r, d, i: o["quadcopter"]["attitude"][:, 1],
+                 lambda o, r, d, i: r.view(2, 3), lambda o, r, d, i: [d]):
+        kept = hold(pick)
+        assert not fr.recyclable()
+        del kept
+        assert fr.recyclable()
+    # a tensor copied out holds nothing
+    c = hold(lambda o, r, d, i: o["quadcopter"]["position"].clone())
+    assert fr.recyclable() and c.shape == (6, 3)
+
+
+def test_frame_pool_cycles_released_frames_only():
+    """FramePool.take: a loop that drops each step's results cycles through
+    two frames; a held Frame object or a held result keeps its frame out."""
+    pool = FramePool(4, torch.device("cpu"), size=3)
+    cur = None
+    seen = []
+    for _ in range(6):  # the env's loop: write a frame, hand out its results, drop the last ones
+        fr = pool.take(cur)
+        out = fr.step_result()
+        cur = fr
+        seen.append(id(fr))
+        del fr, out
+    assert len(set(seen)) == 2 and len(pool.frames) == 2
+    held = pool.take(cur)  # the caller keeps the Frame object itself
+    held.step_result()
+    nxt = pool.take(held)
+    assert nxt is not held and nxt is not cur
+    keep = nxt.step_result()[0]  # ... or an observation
+    a = pool.take(nxt)
+    assert a is not held and a is not nxt
+    assert len(pool.frames) <= 3
+    del keep, held, a
 
 
 def test_action_tensor_forms():
