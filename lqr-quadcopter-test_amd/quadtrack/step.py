@@ -208,6 +208,23 @@ class FramePool:
         return fr
 
 
+class _Out:
+    """A [rows, n] output buffer handed out as its [n, rows] transpose;
+    reusable once released (no reference to the view, no other tensor on
+    the storage), as Frame.recyclable."""
+
+    __slots__ = ("buf", "view", "_ref", "_uses")
+
+    def __init__(self, rows: int, n: int, device):
+        self.buf = torch.empty(rows, n, dtype=F64, device=device)
+        self.view = self.buf.T
+        self._ref = sys.getrefcount(self.view)
+        self._uses = _storage_uses(self.buf)
+
+    def free(self) -> bool:
+        return _CAN_RECYCLE and sys.getrefcount(self.view) == self._ref and _storage_uses(self.buf) == self._uses
+
+
 def tensor_view(t: torch.Tensor, rows: int, n: int, name: str, device) -> View:
     """qt_view of an [n, rows] float64 tensor on `device` (any strides)."""
     if not isinstance(t, torch.Tensor) or t.dtype != F64 or t.device != device or tuple(t.shape) != (n, rows):
@@ -323,12 +340,27 @@ class BatchedControlMixin:
         else:
             v, keep = obs_view_of(obs, n, self.device, self.k_cols == 3)
         integ = self._state_for(n)
-        act = torch.empty(4, n, dtype=F64, device=self.device)
+        out = self._action_out(n)
         check(_abi.load().qt_compute_action_obs(self._ctrl_ref, self._cb_ref, C.byref(v),
-                                                None if integ is None else integ.data_ptr(), act.data_ptr(), None,
+                                                None if integ is None else integ.data_ptr(), out.buf.data_ptr(), None,
                                                 raw_stream(self.device)), "qt_compute_action_obs")
         del keep
-        return act.T
+        return out.view
+
+    def _action_out(self, n: int) -> _Out:
+        """An action buffer the caller no longer holds (the last step's command
+        once env.step has taken it), else a new one; at most three are kept."""
+        outs = self.__dict__.setdefault("_outs", [])
+        if outs and outs[0].buf.shape[1] != n:
+            outs.clear()
+        for o in outs:
+            if o.free():
+                return o
+        o = _Out(4, n, self.device)
+        if len(outs) >= 3:
+            outs.pop(0)
+        outs.append(o)
+        return o
 
 
 def frame_done(fr: Frame) -> torch.Tensor:

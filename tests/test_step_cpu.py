@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from quadtrack import _abi
-from quadtrack.step import Frame, FramePool, action_tensor, frame_words, obs_view_of
+from quadtrack.step import Frame, FramePool, _Out, action_tensor, frame_words, obs_view_of
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 64, 1001])
@@ -114,6 +114,18 @@ def test_frame_pool_cycles_released_frames_only():
     assert a is not held and a is not nxt
     assert len(pool.frames) <= 3
     del keep, held, a
+
+
+def test_action_buffer_reused_only_when_released():
+    o = _Out(4, 5, torch.device("cpu"))
+    assert o.free() and o.view.shape == (5, 4) and o.view.data_ptr() == o.buf.data_ptr()
+    v = o.view
+    assert not o.free()
+    del v
+    w = o.view[:, 0]  # a view derived from the handed-out one
+    assert not o.free()
+    del w
+    assert o.free()
 
 
 def test_action_tensor_forms():
