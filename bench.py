@@ -404,6 +404,7 @@ def main():
 # the done flag, and the linear pattern (3); it writes the new frame
 # (25 doubles, 3 counters, 5 flags) and the action (4 doubles).
 STEP_API_BYTES = (12 + 6 + 1 + 3) * 8 + 1 + 3 * 8 + (25 + 3) * 8 + 5 + 4 * 8
+SURVEY_STEP_BYTES = 200  # x[12] read + write + err
 
 
 def step_api_leg(args, cfg, dev):
@@ -442,6 +443,10 @@ def step_api_leg(args, cfg, dev):
            "env_steps_per_s": round(n / (ms * 1e-3), 1), "host_us_per_step": round(host_s / k * 1e6, 2),
            "contract_bytes_per_env_step": STEP_API_BYTES, "hbm_GBps": round(gbps, 1),
            "hbm_frac": round(gbps / HBM_PEAK_GBS, 4),
+           # SURVEY §8(d)'s nominal B_step (state in and out + the error, 200 B for LQR):
+           # env-steps/s x 200 B / peak; the frame moves the observation and info besides
+           "survey_bytes_per_env_step": SURVEY_STEP_BYTES,
+           "survey_hbm_frac": round(SURVEY_STEP_BYTES * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "kernel": "closed_step_kernel<6, no-FF, structured K, freeze> (qt_frame_closed_step)"}
     del env, ctl
     torch.cuda.empty_cache()

@@ -196,10 +196,22 @@ class FramePool:
         self.n, self.device, self.size = n, device, size
         self.frames: list[Frame] = []
 
+    @staticmethod
+    def _own_refs(items) -> int:
+        # the reference count of an item nothing else holds, seen from take()'s
+        # loop (the list, the loop variable, getrefcount's argument: 3 on CPython)
+        for it in items:
+            return sys.getrefcount(it)
+        return 0
+
+    _OWN = None
+
     def take(self, cur: Frame | None) -> Frame:
+        if FramePool._OWN is None:
+            FramePool._OWN = self._own_refs([object()])
+        own = FramePool._OWN
         for fr in self.frames:
-            # references to fr here: the list, the loop variable, getrefcount's argument
-            if fr is not cur and sys.getrefcount(fr) == 3 and fr.recyclable():
+            if fr is not cur and sys.getrefcount(fr) == own and fr.recyclable():
                 return fr
         fr = Frame(self.n, self.device)
         if len(self.frames) >= self.size:

@@ -6,6 +6,7 @@
 #   bench  scripts/step_api_bench.py at 65,536 and 1,048,576 episodes, both modes, LQR and LQI
 #   trace  rocprofv3 kernel trace + stats of the bench loop (1,048,576 and 65,536 episodes, 3,000 steps)
 #   pmc    FETCH_SIZE and WRITE_SIZE passes of the same loop (1,048,576 and 65,536 episodes, 300 steps)
+#   sq     SQ and F64 passes of the closed step at 1,048,576 episodes (VALU / FP64 issue beside HBM)
 #   exact  the exact step at 65,536 linear LQR episodes (scripts/flavour_timing.py --cases exact):
 #          timing, kernel trace, SQ / SQ2 / F64 passes
 # Outputs under gpurun_out/$TAG/.  The first failing step ends the session.
@@ -40,6 +41,13 @@ for step in ${STEPS:-tests bench}; do
                $(find $O/pmc_${P}_$n -name "*counter_collection.csv")
            done
          done ;;
+    sq) for P in "$SQ" "$F64"; do  # the closed step at 1,048,576 episodes: VALU and FP64 issue
+          name=$(echo $P | tr ' ' '_')
+          timeout -k 10 -s KILL 300 rocprofv3 --pmc $P --output-format csv -d $O/sq_$name -o run -- \
+            python3 scripts/step_api_bench.py --mode closed --ctl lqr --n 1048576 --steps 300 --warm 5 \
+            > $O/sq_$name.log 2>&1 || fail sq $O/sq_$name.log
+        done
+        python3 scripts/pmc_summary.py $O/step_api_pmc_SQ_F64.csv $(find $O/sq_* -name "*counter_collection.csv") ;;
     exact) timeout -k 10 300 python -u scripts/flavour_timing.py --cases exact yaw0 > $O/exact_timing.jsonl 2> $O/exact.err \
              || fail exact $O/exact.err
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/exact_trace -o run -- \
