@@ -13,8 +13,11 @@
 // quadcopter_env.py:481-486) and no copy is made for it.
 //
 // Bound: HBM.  One lane per episode, every load and store a coalesced
-// 512-byte wave access; the exact step's arithmetic (staged RK4, the
-// reference's control flow) is ~1/3 of the memory time at 16 waves per SIMD.
+// 512-byte wave access.  The exact step's arithmetic (staged RK4, the
+// reference's control flow: ~1,000 VALU per episode-step) keeps the SIMDs
+// ~25% busy at 160 VGPRs, three waves per SIMD (DESIGN §3 "Per-step API":
+// 0.57 of HBM at 1,048,576 episodes; fewer registers spill, a lighter step
+// needs more of them).
 // Reference functions: src/quadcopter_tracking/... of the reference repo.
 #include "qt_kernels.hpp"
 
