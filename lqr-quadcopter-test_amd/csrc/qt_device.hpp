@@ -1071,25 +1071,6 @@ __device__ __forceinline__ bool parse_action(const qt_env_params& e, const doubl
   return viol;
 }
 
-// _check_termination (quadcopter_env.py:513-535) as selects.  A finite sum of
-// the 12 components proves them all finite; a non-finite sum (a wave-uniform
-// branch) falls back to the element test.
-__device__ __forceinline__ int termination(const qt_env_params& e, double t, const double* x) {
-  const bool tl = t >= e.max_episode_time;
-  const bool pb = fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) > e.max_position;
-  double sum = 0.0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) sum += x[i];
-  bool fin = isfinite(sum);
-  if (any_lane(!fin)) {
-    bool f = true;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) f = f && isfinite(x[i]);
-    fin = fin || f;
-  }
-  return tl ? QT_TERM_TIME_LIMIT : (pb ? QT_TERM_POSITION_BOUNDS : (fin ? QT_TERM_RUNNING : QT_TERM_NUMERICAL_INSTABILITY));
-}
-
 // ------------------------------------------------- fast-path preconditions
 //
 // The fused rollout has a branch-light variant of the step (the "fast path")
