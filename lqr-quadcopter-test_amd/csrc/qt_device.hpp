@@ -732,7 +732,9 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
 // RK4 up to the rounding of the reassociation (~1e-16 relative per step), as
 // the yaw-at-rest step.  Out: the fourth stage's offsets d4 and trig t4
 // (carry_attitude_trig).  Euler (make_rate_lin / make_vel_lin's one-stage
-// coefficients): stages 2 and 3 carry zero weight and are skipped.
+// coefficients): stages 2 and 3 carry zero weight and are skipped.  RK4: the
+// caller knows integrator == "rk4" (no uniform branch on it per step).
+template <bool RK4 = false>
 __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const RateLin& R, const VelLin& L,
                                                  const Plant& pl, const Trig& ta, double* x, const double* u,
                                                  double* d4, Trig& t4) {
@@ -748,7 +750,7 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   t[0] = ta;
   trig_shift<true>(x + 6, ta, d4, t[3]);
   double em = 0.0;
-  if (e.integrator != 1) {
+  if (RK4 || e.integrator != 1) {
     trig_shift<true>(x + 6, ta, d2, t[1]);
     // the third stage from the second by e3 = d3 - d2 = O(dt^2) (resid_sincos)
 #pragma unroll
@@ -796,7 +798,7 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
     }
   };
   add_stage(t[0], L.wv[0], L.pa[0], true);
-  if (e.integrator != 1) {  // RK4: stages 2 and 3 (uniform)
+  if (RK4 || e.integrator != 1) {  // RK4: stages 2 and 3 (uniform)
     add_stage(t[1], L.wv[1], L.pa[1], true);
     add_stage(t[2], L.wv[2], L.pa[2], true);
   }
