@@ -64,16 +64,30 @@ struct Counts {
   int64_t step, viol, on;
 };
 
+// An episode's per-launch inputs outside the frame: motion type, target
+// pattern, plant.  Loaded with everything else before any data-dependent
+// branch, so that a step waits for memory once (DESIGN §3 "Per-step API").
+struct EpisodeIn {
+  int motion;
+  Pattern pt;
+  Plant pl;
+};
+
+__device__ __forceinline__ EpisodeIn episode_in(const qt_env_params& e, const BatchDev& b, int64_t ep) {
+  const int motion = motion_of(b, e, ep);
+  return EpisodeIn{motion, pattern_of(b, e, motion, ep), make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass)};
+}
+
 // QuadcopterEnv.step (quadcopter_env.py:152-232) of episode ep from state x
 // at time t with the raw action u, into frame O: _parse_and_validate_action
 // (234-293), _integrate (295-327), _apply_state_constraints (428-465),
 // t += dt (191), observation (472-496), reward (504-511), termination
 // (513-535), on-target count (204-207), info (209-226), success (537-553).
-__device__ __forceinline__ void env_step_into(const qt_env_params& e, const BatchDev& b, int64_t n, int64_t ep,
+__device__ __forceinline__ void env_step_into(const qt_env_params& e, const EpisodeIn& in, int64_t n, int64_t ep,
                                               double* x, double t, Counts k, const double* u, const FrameDev& O) {
-  const int motion = motion_of(b, e, ep);
-  const Pattern pt = pattern_of(b, e, motion, ep);
-  const Plant pl = make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
+  const int motion = in.motion;
+  const Pattern& pt = in.pt;
+  const Plant& pl = in.pl;
   double ua[4];
   const bool viol = parse_action(e, u, ua);
   integrate(e, pl, x, ua);
@@ -113,28 +127,25 @@ __device__ __forceinline__ void env_step_into(const qt_env_params& e, const Batc
 // (nine) per-axis gains are read, which equals K s exactly for a finite s;
 // a non-finite observation or integral takes the dense product, whose
 // 0 * NaN terms the reference's K @ s has (riccati_lqr.py:864-900).
+template <int KC, bool KS>
+using CtlGains = Gains<KC, KC == 3 || KS>;
+
 template <int KC, bool FF, bool KS>
-__device__ __forceinline__ bool control(const qt_ctrl_params& c, const BatchDev& b, int64_t ep, double hover,
-                                        const double* qp, const double* qv, const Target& tg, double now,
-                                        const FFLane& fl, double* in, double* u) {
+__device__ __forceinline__ bool control(const qt_ctrl_params& c, const BatchDev& b, int64_t ep,
+                                        const CtlGains<KC, KS>& G, double hover, const double* qp, const double* qv,
+                                        const Target& tg, double now, const FFLane& fl, double* in, double* u) {
   if constexpr (KC == 3) {
-    Gains<3, true> G;
-    load_gains<3, true>(b, ep, G);
     compute_action_pid<FF>(c, G.k, hover, qp, qv, tg, now, fl, in, u);
     return false;
+  } else if constexpr (KS) {
+    double s = ((qp[0] + qp[1]) + (qp[2] + qv[0])) + ((qv[1] + qv[2]) + (tg.p[0] + tg.p[1])) +
+               ((tg.p[2] + tg.v[0]) + (tg.v[1] + tg.v[2]));
+    if (KC == 9) s += (in[0] + in[1]) + in[2];
+    if (__builtin_expect(isfinite(s), 1)) return compute_action<KC, FF, true>(c, G, hover, qp, qv, tg, fl, in, u);
+    Gains<KC, false> D;
+    load_gains<KC, false>(b, ep, D);
+    return compute_action<KC, FF, false>(c, D, hover, qp, qv, tg, fl, in, u);
   } else {
-    if constexpr (KS) {
-      double s = ((qp[0] + qp[1]) + (qp[2] + qv[0])) + ((qv[1] + qv[2]) + (tg.p[0] + tg.p[1])) +
-                 ((tg.p[2] + tg.v[0]) + (tg.v[1] + tg.v[2]));
-      if (KC == 9) s += (in[0] + in[1]) + in[2];
-      if (__builtin_expect(isfinite(s), 1)) {
-        Gains<KC, true> G;
-        load_gains<KC, true>(b, ep, G);
-        return compute_action<KC, FF, true>(c, G, hover, qp, qv, tg, fl, in, u);
-      }
-    }
-    Gains<KC, false> G;
-    load_gains<KC, false>(b, ep, G);
     return compute_action<KC, FF, false>(c, G, hover, qp, qv, tg, fl, in, u);
   }
 }
@@ -186,17 +197,21 @@ __global__ __launch_bounds__(kBlock) void frame_step_kernel(qt_env_params e, Bat
   const int64_t n = b.n;
   if (ep >= n) return;
   const FrameDev I = frame_of(in, n), O = frame_of(out, n);
-  if (FREEZE && I.b[QT_FB_DONE * n + ep]) {
-    if (!inplace) copy_column(I, O, n, ep);
-    return;
-  }
+  // every load before the first data-dependent branch (one memory latency)
+  const bool done = FREEZE && I.b[QT_FB_DONE * n + ep];
   double x[12], u[4];
 #pragma unroll
   for (int i = 0; i < 12; ++i) x[i] = I.f[(QT_FR_X + i) * n + ep];
 #pragma unroll
   for (int i = 0; i < 4; ++i) u[i] = view_at(a, i, ep);
+  const double t = I.f[QT_FR_TIME * n + ep];
   const Counts k{I.c[QT_FC_STEP * n + ep], I.c[QT_FC_VIOLATIONS * n + ep], I.c[QT_FC_ON_TARGET * n + ep]};
-  env_step_into(e, b, n, ep, x, I.f[QT_FR_TIME * n + ep], k, u, O);
+  const EpisodeIn ei = episode_in(e, b, ep);
+  if (done) {
+    if (!inplace) copy_column(I, O, n, ep);
+    return;
+  }
+  env_step_into(e, ei, n, ep, x, t, k, u, O);
 }
 
 // --------------------------------------------------- controller on a view
@@ -222,7 +237,9 @@ __global__ __launch_bounds__(kBlock) void action_obs_kernel(qt_ctrl_params c, Ba
 #pragma unroll
   for (int i = 0; i < NI; ++i) in[i] = integ[i * n + ep];
   const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
-  const bool sat = control<KC, FF, KS>(c, b, ep, hover, qp, qv, tg, now, ff_of(b, c, ep), in, u);
+  CtlGains<KC, KS> G;
+  load_gains<KC, KC == 3 || KS>(b, ep, G);
+  const bool sat = control<KC, FF, KS>(c, b, ep, G, hover, qp, qv, tg, now, ff_of(b, c, ep), in, u);
 #pragma unroll
   for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
 #pragma unroll
@@ -244,14 +261,9 @@ __global__ __launch_bounds__(kBlock) void closed_step_kernel(qt_env_params e, qt
   const int64_t n = b.n;
   if (ep >= n) return;
   const FrameDev I = frame_of(in, n), O = frame_of(out, n);
-  if (FREEZE && I.b[QT_FB_DONE * n + ep]) {
-    if (!inplace) copy_column(I, O, n, ep);
-    if (action) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) action[i * n + ep] = 0.0;
-    }
-    return;
-  }
+  // every load before the first data-dependent branch (the done test, the
+  // controller's finiteness test): one memory latency per step, not three
+  const bool done = FREEZE && I.b[QT_FB_DONE * n + ep];
   constexpr int NI = integ_rows<KC>();
   double x[12], in4[4] = {0.0, 0.0, 0.0, NAN}, u[4];
   Target tg;
@@ -268,15 +280,27 @@ __global__ __launch_bounds__(kBlock) void closed_step_kernel(qt_env_params e, qt
 #pragma unroll
   for (int i = 0; i < NI; ++i) in4[i] = integ[i * n + ep];
   const double hover = b.hover ? b.hover[ep] : c.hover_thrust;
+  CtlGains<KC, KS> G;
+  load_gains<KC, KC == 3 || KS>(b, ep, G);
+  const FFLane fl = ff_of(b, c, ep);
+  const EpisodeIn ei = episode_in(e, b, ep);
+  if (done) {
+    if (!inplace) copy_column(I, O, n, ep);
+    if (action) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) action[i * n + ep] = 0.0;
+    }
+    return;
+  }
   // the observation time is the env time (quadcopter_env.py:495)
-  control<KC, FF, KS>(c, b, ep, hover, x, x + 3, tg, t, ff_of(b, c, ep), in4, u);
+  control<KC, FF, KS>(c, b, ep, G, hover, x, x + 3, tg, t, fl, in4, u);
 #pragma unroll
   for (int i = 0; i < NI; ++i) integ[i * n + ep] = in4[i];
   if (action) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) action[i * n + ep] = u[i];
   }
-  env_step_into(e, b, n, ep, x, t, k, u, O);
+  env_step_into(e, ei, n, ep, x, t, k, u, O);
 }
 
 // ------------------------------------------------------------- dispatch
