@@ -10,7 +10,9 @@ options that used to leave the fast path included (VERDICT r03 missing #2):
   exact       the exact step: every episode starts with a 1e-300 rad/s yaw
               rate, so no wave passes the yaw-at-rest wave test and all go to
               the exact pass (trajectories differ by ~1e-300);
-  exact_euler, exact_rewards  the same for Euler and for rewards.
+  exact_euler, exact_rewards  the same for Euler and for rewards;
+  fast_yaw    a gain with a yaw-rate row (the heuristic LQR's K plus two yaw
+              terms): the full-gain fast flavour (kFast).
 
 HIP events on the launch stream around the reset + rollout launch set,
 median of --reps after a 1 s warm-up.  One JSON line per case.
@@ -43,7 +45,7 @@ def main():
     import torch
 
     from quadtrack import _abi, core
-    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.controllers import BatchedLQR, BatchedRiccatiLQR
     from quadtrack.env.config import EnvConfig
     from quadtrack.rollout import build_batch, max_steps_for
 
@@ -93,6 +95,37 @@ def main():
                 print(json.dumps({"case": name, "integrator": integrator, "rewards": rewards, "n": n,
                                   "motion": args.motion, "ms": round(ms, 4), "ms_min": round(min(times), 4),
                                   "env_steps_per_s": round(done / (ms * 1e-3), 1)}), flush=True)
+    if args.cases is None or "fast_yaw" in args.cases:
+        K = BatchedLQR({}).gains()[0].cpu().numpy().copy()
+        K[3, 0], K[3, 4] = 0.02, -0.01
+        yctl = BatchedLQR({"K": K}, device=dev)
+        cfg = EnvConfig.from_dict({"target": {"motion_type": args.motion}})
+        env = cfg.to_params()
+        batch = build_batch(yctl, cfg, n, seeds=np.arange(n))
+        steps = max_steps_for(env)
+        st = core.RolloutState.empty(n, dev)
+
+        def one_yaw():
+            core.reset(env, batch, st)
+            core.rollout(env, yctl.ctrl, crit, batch, st, steps)
+
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.warmup_s:
+            one_yaw()
+            torch.cuda.synchronize()
+        times = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            one_yaw()
+            e1.record(s)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        ms = float(np.median(times))
+        done = float(st.acc[_abi.ACC_STEPS].sum().item())
+        print(json.dumps({"case": "fast_yaw", "integrator": "rk4", "rewards": False, "n": n, "motion": args.motion,
+                          "ms": round(ms, 4), "ms_min": round(min(times), 4),
+                          "env_steps_per_s": round(done / (ms * 1e-3), 1)}), flush=True)
 
 
 if __name__ == "__main__":
