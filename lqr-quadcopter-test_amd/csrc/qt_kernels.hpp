@@ -293,16 +293,13 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   // last step's tracking error (info["tracking_error"], train.py:630)
   double rew_sum = 0.0, rew_last = 0.0;
   if (!FAST && reward) rew_sum = reward[ep], rew_last = reward[n + ep];
-  // the exact step: closed-form RK4 / Euler (integrate_closed) with sin / cos
-  // of the attitude carried across steps (carry_attitude_trig)
+  // closed-form RK4 / Euler (integrate_closed) with sin / cos of the attitude
+  // carried across steps (carry_attitude_trig): the exact step, and the
+  // full-gain fast step (kFast, whose launch knows the integrator is RK4)
   Trig ta;
-  RateLin rl{};
-  VelLin vl{};
-  if (!FAST) {
-    trig_of(x + 6, ta);
-    rl = make_rate_lin(e);
-    vl = make_vel_lin(e, pl);
-  }
+  trig_of(x + 6, ta);
+  const RateLin rl = make_rate_lin(e);
+  const VelLin vl = make_vel_lin(e, pl);
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -344,7 +341,9 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
     // ---- env.step (quadcopter_env.py:152-232)
     if (FAST) {
       // the command is finite and inside the env clamps: parsing is the identity
-      integrate<true, false>(e, pl, x, u);
+      double a0[3] = {x[6], x[7], x[8]}, d4[3];
+      Trig t4;
+      integrate_closed<true>(e, rl, vl, pl, ta, x, u, d4, t4);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kCarry)
@@ -368,6 +367,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
         a.on_post += norm_le(se, e.target_radius);
       }
+      carry_attitude_trig(a0, x + 6, d4, t4, ta);
       if (QT_ABLATE & QT_ABL_TERMINATION)
         a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
       else
