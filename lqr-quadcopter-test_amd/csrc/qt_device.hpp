@@ -817,21 +817,17 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   }
 }
 
-// _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327); u is held
-// constant across the four stages.
-// FAST: RK4 known (integrator == 0) and every stage offset proven small.
-// YAW0 (with FAST): yaw identically zero; x[8] and x[11] are left untouched.
-template <bool FAST = false, bool YAW0 = false>
+// _integrate / _rk4_step / _euler_step (quadcopter_env.py:295-327), stage by
+// stage as the reference evaluates it; u is held constant across the four
+// stages.  The per-step API's env.step (any caller-supplied state, overflow
+// and NaN propagation as numpy's); the rollout's steps use integrate_closed.
 __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& pl, double* x, const double* u) {
-  static_assert(FAST || !YAW0, "YAW0 is a fast-path specialisation");
-  // state components that evolve (YAW0: all but yaw 8 and yaw rate 11)
-  auto live = [](int i) { return !YAW0 || (i != 8 && i != 11); };
   const double dt = e.dt;
   double k[12];
   Trig t0, ts;
-  trig_of<YAW0>(x + 6, t0);
-  derivatives<YAW0>(e, pl, x, u, t0, k);
-  if (!FAST && e.integrator == 1) {
+  trig_of(x + 6, t0);
+  derivatives(e, pl, x, u, t0, k);
+  if (e.integrator == 1) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = x[i] + k[i] * dt;
     return;
@@ -839,43 +835,38 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
   // Stage states.  Their angles only enter through sin/cos (derivatives of
   // the angles are the body rates), so stage trig is the step-start trig
   // shifted by the stage offset h * k[6..8].
-  double acc[12], tmp[12], del[3] = {0.0, 0.0, 0.0};
+  double acc[12], tmp[12], del[3];
   const double h2 = 0.5 * dt;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
-    if (!live(i)) continue;
     acc[i] = k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
-  if (YAW0) tmp[8] = tmp[11] = 0.0;
 #pragma unroll
-  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = h2 * k[6 + i];
-  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
-  derivatives<YAW0>(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
-    if (!live(i)) continue;
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + h2 * k[i];
   }
 #pragma unroll
-  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = h2 * k[6 + i];
-  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
-  derivatives<YAW0>(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < 3; ++i) del[i] = h2 * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
-    if (!live(i)) continue;
     acc[i] = acc[i] + 2.0 * k[i];
     tmp[i] = x[i] + dt * k[i];
   }
 #pragma unroll
-  for (int i = 0; i < (YAW0 ? 2 : 3); ++i) del[i] = dt * k[6 + i];
-  trig_shift<FAST, YAW0>(x + 6, t0, del, ts);
-  derivatives<YAW0>(e, pl, tmp, u, ts, k);
+  for (int i = 0; i < 3; ++i) del[i] = dt * k[6 + i];
+  trig_shift(x + 6, t0, del, ts);
+  derivatives(e, pl, tmp, u, ts, k);
   const double h6 = dt / 6.0;
 #pragma unroll
-  for (int i = 0; i < 12; ++i)
-    if (live(i)) x[i] = x[i] + h6 * (acc[i] + k[i]);
+  for (int i = 0; i < 12; ++i) x[i] = x[i] + h6 * (acc[i] + k[i]);
 }
 
 // The exact step's carried attitude trig: sin / cos of the constrained new
