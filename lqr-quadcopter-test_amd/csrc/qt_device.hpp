@@ -732,9 +732,10 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
 // RK4 up to the rounding of the reassociation (~1e-16 relative per step), as
 // the yaw-at-rest step.  Out: the fourth stage's offsets d4 and trig t4
 // (carry_attitude_trig).  Euler (make_rate_lin / make_vel_lin's one-stage
-// coefficients): stages 2 and 3 carry zero weight and are skipped.  RK4: the
-// caller knows integrator == "rk4" (no uniform branch on it per step).
-template <bool RK4 = false>
+// coefficients): stages 2 and 3 carry zero weight and are skipped.  INTEG:
+// the integrator when the caller knows it at compile time (0 "rk4", 1
+// "euler": no uniform branch on it per step), -1 read from e.
+template <int INTEG = -1>
 __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const RateLin& R, const VelLin& L,
                                                  const Plant& pl, const Trig& ta, double* x, const double* u,
                                                  double* d4, Trig& t4) {
@@ -750,7 +751,7 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   t[0] = ta;
   trig_shift<true>(x + 6, ta, d4, t[3]);
   double em = 0.0;
-  if (RK4 || e.integrator != 1) {
+  if (INTEG == 0 || (INTEG < 0 && e.integrator != 1)) {
     trig_shift<true>(x + 6, ta, d2, t[1]);
     // the third stage from the second by e3 = d3 - d2 = O(dt^2) (resid_sincos)
 #pragma unroll
@@ -798,7 +799,7 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
     }
   };
   add_stage(t[0], L.wv[0], L.pa[0], true);
-  if (RK4 || e.integrator != 1) {  // RK4: stages 2 and 3 (uniform)
+  if (INTEG == 0 || (INTEG < 0 && e.integrator != 1)) {  // RK4: stages 2 and 3 (uniform)
     add_stage(t[1], L.wv[1], L.pa[1], true);
     add_stage(t[2], L.wv[2], L.pa[2], true);
   }

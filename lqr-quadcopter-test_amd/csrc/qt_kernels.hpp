@@ -263,7 +263,7 @@ __device__ __forceinline__ double sq3_ref(double a, double b, double c) {
 // takes the exact step's decisions; rare lanes/steps (speed at the
 // clamp, attitude far outside [-pi, pi), tracking error at the radius within
 // 1e-14) fall back to the exact constraint / comparison code inside the step.
-template <bool FAST, int MOTION, int KC, bool FF, bool KS, bool RK4 = false>
+template <bool FAST, int MOTION, int KC, bool FF, bool KS, int INTEG = -1>
 __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl, double hover,
                                           const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
@@ -343,7 +343,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       // the command is finite and inside the env clamps: parsing is the identity
       double a0[3] = {x[6], x[7], x[8]}, d4[3];
       Trig t4;
-      integrate_closed<true>(e, rl, vl, pl, ta, x, u, d4, t4);
+      integrate_closed<0>(e, rl, vl, pl, ta, x, u, d4, t4);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kCarry)
@@ -377,7 +377,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       double ua[4], a0[3] = {x[6], x[7], x[8]}, d4[3];
       a.viol += parse_action(e, u, ua);
       Trig t4;
-      integrate_closed<RK4>(e, rl, vl, pl, ta, x, ua, d4, t4);
+      integrate_closed<INTEG>(e, rl, vl, pl, ta, x, ua, d4, t4);
       t += e.dt;
       const int term = constrain_terminate<false>(e, x, t);
       carry_attitude_trig(a0, x + 6, d4, t4, ta);
@@ -854,10 +854,10 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // register budget has no room, and its fresh passes take qt_reset and
 // metrics_kernel around the launch).
 // REC (the exact flavour): the launch may record steps (rec) or keep rewards
-// (lc.reward); without them the exact loop carries neither pointer.  RK4 (the
-// exact flavour): integrator == "rk4" is known at launch (integrate_closed).
+// (lc.reward); without them the exact loop carries neither pointer.  INTEG
+// (the exact flavour): the integrator, known at launch (integrate_closed).
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true, bool REC = true,
-          bool RK4 = false>
+          int INTEG = -1>
 __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                              const BatchDev& b, const qt_state& st, int nsteps,
                                              double* __restrict__ rec, int deferred, const LaunchConst& lc,
@@ -995,7 +995,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     }
   } else {
     if (deferred != kExact && wave_ok) return;
-    run_steps<false, MOTION, KC, FF, KS, RK4>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
+    run_steps<false, MOTION, KC, FF, KS, INTEG>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
                                          REC ? rec : nullptr, n, ep, REC ? lc.reward : nullptr);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
@@ -1012,7 +1012,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   if (FRESH && lc.met) store_metrics(cr, a, t, lc.met, n, ep);  // a fresh pass: the metrics rows (metrics_kernel)
 }
 
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool REC = true, bool RK4 = false>
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool REC = true, int INTEG = -1>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   if (FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch) return;
   const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
   if (slot < 0) return;
-  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI, true, REC, RK4>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
+  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI, true, REC, INTEG>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
 }
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type

@@ -550,20 +550,22 @@ struct ExactLaunch {
   static void run(int deferred, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                   const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec,
                   const LaunchConst& lc) {
-    if (e.integrator == 0)  // RK4 known: no per-step branch on the integrator
-      launch<MOTION, KC, FF, KS, true>(deferred, grid, s, e, c, cr, b, st, nsteps, rec, lc);
+    // the integrator known at compile time: no per-step branch on it (any
+    // value but "euler" steps RK4, as integrate_closed reads it at run time)
+    if (e.integrator == 1)
+      launch<MOTION, KC, FF, KS, 1>(deferred, grid, s, e, c, cr, b, st, nsteps, rec, lc);
     else
-      launch<MOTION, KC, FF, KS, false>(deferred, grid, s, e, c, cr, b, st, nsteps, rec, lc);
+      launch<MOTION, KC, FF, KS, 0>(deferred, grid, s, e, c, cr, b, st, nsteps, rec, lc);
   }
-  template <int MOTION, int KC, bool FF, bool KS, bool RK4>
+  template <int MOTION, int KC, bool FF, bool KS, int INTEG>
   static void launch(int deferred, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                      const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec,
                      const LaunchConst& lc) {
     if (rec || lc.reward)
-      rollout_kernel<kExact, MOTION, KC, FF, KS, false, true, RK4><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, true, INTEG><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
                                                                                           rec, deferred, lc);
     else  // no recording, no rewards: the loop without either pointer
-      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false, RK4><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false, INTEG><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
                                                                                            nullptr, deferred, lc);
   }
 };
