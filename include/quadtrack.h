@@ -320,7 +320,13 @@ int qt_rollout_rewards(const qt_env_params* env, const qt_ctrl_params* ctrl, con
    batch->motion (when given) for every slot; a wave holding a slot whose
    batch->motion differs is run by the exact pass, which takes each episode's
    motion from batch->motion — in the one-launch grouped flavour and in the
-   per-segment launch sets alike. */
+   per-segment launch sets alike.  Stationary riders (one-launch flavour, with
+   batch->motion given; QT_RIDERS=0 in the environment turns them off): the
+   first episodes of the stationary group fill the free lanes of every other
+   group's last wave (the group's loop with the stationary target selected per
+   lane, the same numbers bit for bit), so N episodes take ceil(N / 64) waves
+   when the stationary group can fill the other groups' gaps (round 6:
+   config 5's 8-GPU shard, 2,050 -> 2,048 waves). */
 int qt_rollout_grouped(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                        const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, int32_t nseg,
                        const int32_t* seg_motion, const int64_t* seg_end, void* stream);

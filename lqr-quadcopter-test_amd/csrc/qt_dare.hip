@@ -868,7 +868,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QT_DARE_ROW_
   double ar[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) ar[j] = a_in(j);
-  double rel_prev = INFINITY;  // the last doubling's |dH|_F^2 / |H|_F^2
+  // the last doubling's |dH|_F^2 / |H|_F^2; NaN before the first doubling, so
+  // the quadratic test below always compares two measured changes (a first
+  // change that happens to be small proves nothing about the convergence rate)
+  double rel_prev = __builtin_nan("");
 
   // ---- doublings: W = I + G H ; Winv = W^-1 ; Y1 = Winv A ; Y2 = Winv G ;
   // H += sym(A' H Y1) ; G += sym(A Y2 A') ; A = A Y1, until |dH|_F <= tol |H|_F

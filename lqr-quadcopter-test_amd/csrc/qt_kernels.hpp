@@ -103,6 +103,14 @@ struct BatchDev {
   int32_t nseg;
   int8_t seg_motion[8];
   int64_t seg_end[8], wave_end[8];
+  // Stationary riders (one-launch grouped rollout, rollout_batch): the free
+  // lanes of a group's last wave take episodes of the stationary group, whose
+  // target (a fixed point) the group's loop forms by a per-lane select
+  // (ride_target).  Group i's waves run its own slots [seg_lo[i], seg_end[i])
+  // and then the riders [ride_lo[i], ride_lo[i] + ride_cnt[i]); the riders come
+  // from the front of the stationary group's slot range, whose own waves start
+  // after them (its seg_lo).  Slot ranges, and so slot_motion, are unchanged.
+  int64_t seg_lo[8], ride_lo[8], ride_cnt[8];
   // A per-segment launch of a grouped batch (qt_rollout_grouped's one launch
   // set per group): the group's motion, which its slots' batch->motion must
   // match (-1: none to check).  A wave holding a slot that does not is left to
@@ -111,22 +119,33 @@ struct BatchDev {
 };
 
 // The slot a launch position runs, or -1 past the launch's slot range (or in
-// the unused tail of a group's last wave).
-__device__ __forceinline__ int64_t slot_at(const BatchDev& b, int64_t p) {
+// the unused tail of a group's last wave); `ride`: the slot is a stationary
+// rider in another group's wave (BatchDev::ride_lo).
+__device__ __forceinline__ int64_t slot_at(const BatchDev& b, int64_t p, bool& ride) {
+  ride = false;
   if (b.nseg == 0) {
     const int64_t slot = b.slot0 + p;
     return slot < b.slot_end ? slot : -1;
   }
   const int64_t w = p >> 6;
-  int64_t s0 = 0, w0 = 0;
+  int64_t w0 = 0;
   for (int i = 0; i < b.nseg; ++i) {  // uniform per wave
     if (w < b.wave_end[i]) {
-      const int64_t slot = s0 + ((w - w0) << 6) + (p & 63);
-      return slot < b.seg_end[i] ? slot : -1;
+      int64_t q = ((w - w0) << 6) + (p & 63);
+      const int64_t own = b.seg_end[i] - b.seg_lo[i];
+      if (q < own) return b.seg_lo[i] + q;
+      q -= own;
+      ride = q < b.ride_cnt[i];
+      return ride ? b.ride_lo[i] + q : -1;
     }
-    s0 = b.seg_end[i], w0 = b.wave_end[i];
+    w0 = b.wave_end[i];
   }
   return -1;
+}
+
+__device__ __forceinline__ int64_t slot_at(const BatchDev& b, int64_t p) {
+  bool ride;
+  return slot_at(b, p, ride);
 }
 
 // The motion of a wave-aligned group's wave (b.nseg > 0), uniform per wave.
@@ -283,7 +302,9 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   // post-step error (positions are not constrained, so they are the same
   // number), ||p - p_T|| in np.linalg.norm(axis=1)'s order (sq3_ref)
   double err_pre = 0.0;
-  if (!FAST) err_pre = sqrt_noscale(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
+  // (sqrt, not sqrt_noscale: a caller's state may hold an infinite position
+  // still marked running, whose error numpy's norm gives as inf; once per launch)
+  if (!FAST) err_pre = sqrt(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
   // fast steps of a periodic pattern carry its angles' sin / cos (target_state_carried)
   constexpr bool kCarry = FAST && (MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_CIRCULAR);
   PeriodicTrig<kCarry ? MOTION : QT_MOTION_CIRCULAR> ptrig;
@@ -635,11 +656,30 @@ constexpr int kDualBelow = 8;  // tilt-bounded horizons shorter than this try th
 #define QT_GROUPED_DUAL 0  // the grouped kernel (two waves per SIMD, 256 VGPRs) too
 #endif
 
-template <int MOTION, int KC, bool FF, bool KS, bool UNI, bool DUAL = false>
+// A stationary rider (BatchDev::ride_lo) in another group's wave: the
+// stationary pattern's observation (target_motion.py:233-246, 387-411: the
+// fixed point, zero velocity and acceleration) in place of what the group's
+// loop formed, by a per-lane select.  The values are the stationary loop's
+// bit for bit, and so is every step built on them (-ffp-contract=on: the
+// same source expressions round alike in every specialised loop).
+template <bool RIDE>
+__device__ __forceinline__ void ride_target(const qt_env_params& e, bool still, Target& tg) {
+  if constexpr (RIDE) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      tg.p[i] = still ? e.center[i] : tg.p[i];
+      tg.v[i] = still ? 0.0 : tg.v[i];
+      tg.a[i] = still ? 0.0 : tg.a[i];
+    }
+  }
+}
+
+template <int MOTION, int KC, bool FF, bool KS, bool UNI, bool DUAL = false, bool RIDE = false>
 __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                          int motion, const Pattern& pt, const Plant& pl_lane, double hover,
                                          const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
-                                         Target& tg, double& t, Acc& a, int nsteps, const LaunchConst& k) {
+                                         Target& tg, double& t, Acc& a, int nsteps, const LaunchConst& k,
+                                         bool still = false) {
   constexpr bool kRotor = MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
                           (MOTION == QT_MOTION_FIGURE8 && !FF);
   constexpr int kNeg = -(1 << 30);
@@ -667,6 +707,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
   } else {
     target_state<FF, true>(e, motion, pt, t, tg);
   }
+  ride_target<RIDE>(e, still, tg);
   double err = sqrt_pos(sq3_ref(tg.p[0] - x[0], tg.p[1] - x[1], tg.p[2] - x[2]));
   Trig ta;
   trig_of<true>(x + 6, ta);
@@ -741,6 +782,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
         } else {
           target_state<FF, true>(e, motion, pt, t, tg);
         }
+        ride_target<RIDE>(e, still, tg);
       }
       // post-step tracking error: the env's on-target count now, the next
       // step's pre-step error (positions are not constrained)
@@ -857,14 +899,20 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // (lc.reward); without them the exact loop carries neither pointer.  INTEG
 // (the exact flavour): the integrator, known at launch (integrate_closed).
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true, bool REC = true,
-          int INTEG = -1>
+          int INTEG = -1, bool RIDE = false>
 __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                              const BatchDev& b, const qt_state& st, int nsteps,
                                              double* __restrict__ rec, int deferred, const LaunchConst& lc,
                                              int64_t slot) {
   const int64_t n = b.n, ep = episode_of(b, slot);
   const int motion = MOTION >= 0 ? MOTION : motion_of(b, e, ep);
-  const Pattern pt = pattern_of(b, e, motion, ep);
+  // RIDE (the grouped kernel's waves with stationary riders): a rider lane
+  // runs the group's loop with the stationary target (ride_target); its
+  // pattern constants are zeroed so the group's target arithmetic, whose
+  // result the select replaces, stays on finite numbers
+  const bool still = RIDE && slot_motion(b, slot) == QT_MOTION_STATIONARY;
+  Pattern pt = pattern_of(b, e, motion, ep);
+  if (RIDE) pt.c0 = still ? 0.0 : pt.c0, pt.c1 = still ? 0.0 : pt.c1, pt.c2 = still ? 0.0 : pt.c2;
   const Plant pl = UNI ? lc.pl : make_plant(e, b.plant_mass ? b.plant_mass[ep] : e.mass);
   const double hover = UNI ? c.hover_thrust : (b.hover ? b.hover[ep] : c.hover_thrust);
   Gains<KC, KS> G;
@@ -971,9 +1019,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     if constexpr (FLAVOR == kYaw0)
       run_yaw0<MOTION, KC, FF, KS, UNI,
                (FRESH || QT_GROUPED_DUAL) && KC != 9 &&
-                   (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL ||
-                    MOTION == QT_MOTION_FIGURE8)>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
-                                                  lc);
+                   (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_FIGURE8),
+               RIDE>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, lc, still);
     else
       run_steps<true, MOTION, KC, FF, KS>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps, rec,
                                           n, ep);
@@ -1005,7 +1052,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     Target full;
     target_state<true>(e, motion, pt, t, full);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) tg.a[i] = full.a[i];
+    for (int i = 0; i < 3; ++i) tg.a[i] = still ? 0.0 : full.a[i];  // a rider's: the stationary target's zero
   }
 
   store_state();
@@ -1038,19 +1085,28 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
 #ifndef QT_GROUPED_WAVES
 #define QT_GROUPED_WAVES 2
 #endif
+#ifndef QT_GROUPED_RIDERS
+#define QT_GROUPED_RIDERS 1  // the rider loops (rollout_batch sets up riders only when this is 1)
+#endif
 template <int KC, bool FF, bool KS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUPED_WAVES))) void rollout_grouped_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                                  BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t slot = slot_at(b, p);
+  bool ride;
+  const int64_t slot = slot_at(b, p, ride);
   if (slot < 0) return;
   const int wm = wave_motion(b, p);
-  if (b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != wm) != 0) {
+  // the motion a lane's slot belongs to (a rider's: stationary), which the
+  // exact pass's wave test compares too (rollout_lane)
+  if (b.motion && __builtin_amdgcn_ballot_w64((int)b.motion[episode_of(b, slot)] != slot_motion(b, slot)) != 0) {
     // a lane's own motion is not its group's: the exact pass runs the wave
     if (lc.defer_flag) *lc.defer_flag = lc.epoch;
     return;
   }
-  switch (wm) {
+  // one switch over (motion, riders): a wave with stationary riders (uniform)
+  // takes its group's loop with the rider select (rollout_lane's RIDE)
+  const int key = wm + ((QT_GROUPED_RIDERS && __builtin_amdgcn_ballot_w64(ride) != 0) ? 8 : 0);
+  switch (key) {
     case QT_MOTION_STATIONARY:
       rollout_lane<kYaw0, QT_MOTION_STATIONARY, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
@@ -1063,8 +1119,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QT_GROUP
     case QT_MOTION_SINUSOIDAL:
       rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
       break;
-    default:
+    case QT_MOTION_FIGURE8:
       rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS, false, false>(e, c, cr, b, st, nsteps, nullptr, kExact, lc, slot);
+      break;
+#if QT_GROUPED_RIDERS
+    case 8 + QT_MOTION_LINEAR:
+      rollout_lane<kYaw0, QT_MOTION_LINEAR, KC, FF, KS, false, false, true, -1, true>(e, c, cr, b, st, nsteps, nullptr,
+                                                                                   kExact, lc, slot);
+      break;
+    case 8 + QT_MOTION_CIRCULAR:
+      rollout_lane<kYaw0, QT_MOTION_CIRCULAR, KC, FF, KS, false, false, true, -1, true>(e, c, cr, b, st, nsteps, nullptr,
+                                                                                     kExact, lc, slot);
+      break;
+    case 8 + QT_MOTION_SINUSOIDAL:
+      rollout_lane<kYaw0, QT_MOTION_SINUSOIDAL, KC, FF, KS, false, false, true, -1, true>(e, c, cr, b, st, nsteps,
+                                                                                       nullptr, kExact, lc, slot);
+      break;
+    case 8 + QT_MOTION_FIGURE8:
+      rollout_lane<kYaw0, QT_MOTION_FIGURE8, KC, FF, KS, false, false, true, -1, true>(e, c, cr, b, st, nsteps, nullptr,
+                                                                                    kExact, lc, slot);
+      break;
+#endif
+    default:  // (no other key: rollout_batch gives a stationary group no riders)
+      break;
   }
 }
 

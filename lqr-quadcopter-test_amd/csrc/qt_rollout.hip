@@ -626,6 +626,45 @@ int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ct
   return fast ? kFast : kExact;
 }
 
+// Stationary riders (BatchDev::ride_lo) in the one-launch grouped rollout:
+// on unless QT_RIDERS=0 (an A/B and test knob, read at each launch).
+bool riders_on() {
+  const char* s = getenv("QT_RIDERS");
+  return !(s && s[0] == '0' && s[1] == '\0');
+}
+
+// The waves of a one-launch grouped rollout (bg's segments: seg_motion,
+// seg_lo = previous seg_end, seg_end) and their wave_end.  With riders, the
+// first episodes of the stationary group fill the free lanes of every other
+// group's last wave, in group order, and the stationary group's own waves
+// start after them: a batch of N episodes then needs ceil(N / 64) waves
+// whenever the stationary group can fill the other groups' gaps (config 5's
+// 131,072-episode 8-GPU shard: 2,048 waves, the resident set at two waves per
+// SIMD, instead of 2,050).  Riders need per-episode motions (batch->motion):
+// the exact pass takes a deferred rider's motion from there.
+int64_t grouped_waves(BatchDev& bg, bool riders) {
+  int stat = -1;
+  for (int i = 0; i < bg.nseg; ++i)
+    if (bg.seg_motion[i] == QT_MOTION_STATIONARY && stat < 0) stat = i;
+  if (riders && stat >= 0) {
+    int64_t next = bg.seg_lo[stat], avail = bg.seg_end[stat] - bg.seg_lo[stat];
+    for (int i = 0; i < bg.nseg; ++i) {
+      if (i == stat) continue;
+      const int64_t gap = (64 - (bg.seg_end[i] - bg.seg_lo[i]) % 64) % 64;
+      const int64_t take = gap < avail ? gap : avail;
+      bg.ride_lo[i] = next, bg.ride_cnt[i] = take;
+      next += take, avail -= take;
+    }
+    bg.seg_lo[stat] = next;
+  }
+  int64_t waves = 0;
+  for (int i = 0; i < bg.nseg; ++i) {
+    waves += (bg.seg_end[i] - bg.seg_lo[i] + bg.ride_cnt[i] + 63) / 64;
+    bg.wave_end[i] = waves;
+  }
+  return waves;
+}
+
 // One rollout launch set: the fast flavour the launch-level preconditions
 // allow, then the exact kernel for the waves it left (or for everything).
 // grouped: b covers a motion-grouped batch in wave-aligned segments and the
@@ -684,22 +723,24 @@ int rollout_batch(const qt_env_params& e, const qt_ctrl_params& c, const qt_crit
     // every group in one launch, each starting at a wavefront boundary (BatchDev's
     // wave-aligned segments; both the fast kernel and its exact pass map slots so)
     BatchDev bg = b;
-    int64_t waves = 0, prev_end = 0;
+    int64_t prev_end = 0;
     bool fits = true;
     for (int32_t i = 0; i < nseg && fits; ++i) {
       const int64_t cnt = seg_end[i] - prev_end;
-      prev_end = seg_end[i];
-      if (cnt == 0) continue;
-      if (bg.nseg == 8) {
-        fits = false;
-        break;
+      if (cnt > 0) {
+        if (bg.nseg == 8) {
+          fits = false;
+          break;
+        }
+        bg.seg_motion[bg.nseg] = (int8_t)seg_motion[i];
+        bg.seg_lo[bg.nseg] = prev_end;
+        bg.seg_end[bg.nseg] = seg_end[i];
+        bg.ride_lo[bg.nseg] = bg.ride_cnt[bg.nseg] = 0;
+        ++bg.nseg;
       }
-      waves += (cnt + 63) / 64;
-      bg.seg_motion[bg.nseg] = (int8_t)seg_motion[i];
-      bg.seg_end[bg.nseg] = seg_end[i];
-      bg.wave_end[bg.nseg] = waves;
-      ++bg.nseg;
+      prev_end = seg_end[i];
     }
+    const int64_t waves = fits ? grouped_waves(bg, QT_GROUPED_RIDERS && batch->motion != nullptr && riders_on()) : 0;
     if (fits) {
       // the grouped kernel has no fresh prologue / epilogue (rollout_lane's FRESH)
       if (fresh_off) reset_kernel<<<grid_of(batch->n), kBlock, 0, s>>>(e, b, fresh_off, st);

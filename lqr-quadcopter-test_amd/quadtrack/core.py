@@ -399,6 +399,45 @@ def motion_groups(motion):
     return order, kinds, [int(v) for v in np.cumsum(counts[kinds])]
 
 
+def riders_on() -> bool:
+    """Stationary riders in the one-launch grouped rollout (qt_rollout.hip
+    riders_on): on unless QT_RIDERS=0."""
+    return os.environ.get("QT_RIDERS") != "0"
+
+
+def grouped_waves(seg_motion, seg_end, riders: bool | None = None) -> int:
+    """The waves of the one-launch grouped rollout of a batch grouped as
+    (seg_motion, seg_end) — qt_rollout.hip grouped_waves restated: with
+    riders, the first episodes of the stationary group fill the free lanes of
+    every other group's last wave, so the stationary group's own waves hold
+    only the rest.  (For reports and tests; the kernel's layout is the C
+    side's.)"""
+    riders = riders_on() if riders is None else riders
+    cnt, prev = [], 0
+    for m, e in zip(seg_motion, seg_end):
+        if e - prev > 0:
+            cnt.append([int(m), int(e - prev), 0])  # motion, own episodes, riders
+        prev = e
+    stat = next((i for i, c in enumerate(cnt) if c[0] == 0), None)
+    if riders and stat is not None:
+        avail = cnt[stat][1]
+        for i, c in enumerate(cnt):
+            if i != stat:
+                take = min((64 - c[1] % 64) % 64, avail)
+                c[2], avail = take, avail - take
+        cnt[stat][1] = avail
+    return sum((own + rid + 63) // 64 for _, own, rid in cnt)
+
+
+def launch_waves(batch: EpisodeBatch) -> int:
+    """Waves of a rollout launch over `batch`: the grouped layout's
+    (grouped_waves) for a motion-grouped batch with per-episode motions,
+    ceil(n / 64) otherwise."""
+    if batch.groups is not None:
+        return grouped_waves(*batch.groups, riders=None if batch.motion is not None else False)
+    return (batch.n + 63) // 64
+
+
 def seed_uniform(seeds: torch.Tensor, lo, hi) -> torch.Tensor:
     """First k draws of default_rng(seed).uniform(lo[j], hi[j]) per seed -> [k, n]."""
     lib = _abi.load()

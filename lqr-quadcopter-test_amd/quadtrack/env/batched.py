@@ -175,6 +175,8 @@ class BatchedQuadcopterEnv:
         is not advanced."""
         fr = self._current()
         n, dev = self.num_envs, self.device
+        if controller.device != dev:
+            raise ValueError(f"the controller is on {controller.device}, the environment on {dev}")
         cb = self._closed_batch(controller)
         integ = controller._state_for(n)
         out = self._next_frame()

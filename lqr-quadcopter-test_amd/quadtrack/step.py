@@ -52,12 +52,16 @@ class Observation(dict):
     __slots__ = ("frame",)
 
 
-def _storage_uses(t: torch.Tensor) -> int:
-    """Tensors (views included) sharing t's storage, +1 for the temporary."""
-    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
-
-
 _CAN_RECYCLE = hasattr(torch._C, "_storage_Use_Count")
+
+
+def _storage_uses(t: torch.Tensor) -> int:
+    """Tensors (views included) sharing t's storage, +1 for the temporary;
+    0 on a torch build without the (private) use count, whose frames and
+    action buffers are then never recycled (_CAN_RECYCLE)."""
+    if not _CAN_RECYCLE:
+        return 0
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
 
 
 class Frame:
@@ -72,7 +76,16 @@ class Frame:
     (a slice, a reshape) shares its storage.  So a caller that keeps an
     observation, a reward, an info value or a view derived from one keeps
     it unchanged, as with a fresh frame; a loop that drops them lets the
-    env cycle through two frames without allocating or building views."""
+    env cycle through two frames without allocating or building views.
+
+    What a held tensor pins: every reward, done, info or observation tensor
+    is a view of the whole frame, so holding one keeps the frame's
+    QT_FRAME_BYTES(n) (229 B per episode) plus its 32 B of command rows alive
+    and out of the recycling cycle.  A loop that keeps a value of every step
+    (the reference Evaluator keeps each step's reward and info,
+    eval.py:139-159) should keep `value.clone()` (8 B per episode), not the
+    view: 65,536 episodes x 3,000 steps of held views would pin ~51 GB where
+    clones take ~1.5 GB."""
 
     __slots__ = ("n", "buf", "f", "c", "b", "act", "ptr", "version", "_q", "_obs_view", "_views", "_refs",
                  "_uses", "_info")
@@ -348,14 +361,17 @@ class BatchedControlMixin:
         fr = getattr(obs, "frame", None)
         keep = None
         if fr is not None and fr.n == n and fr.views_of(obs):
+            if fr.buf.device != self.device:
+                raise ValueError(f"the observation is on {fr.buf.device}, the controller on {self.device}")
             v = fr.obs_view()
         else:
             v, keep = obs_view_of(obs, n, self.device, self.k_cols == 3)
         integ = self._state_for(n)
         out = self._action_out(n)
-        check(_abi.load().qt_compute_action_obs(self._ctrl_ref, self._cb_ref, C.byref(v),
-                                                None if integ is None else integ.data_ptr(), out.buf.data_ptr(), None,
-                                                raw_stream(self.device)), "qt_compute_action_obs")
+        with torch.cuda.device(self.device):  # the launch's stream and pointers are this device's
+            check(_abi.load().qt_compute_action_obs(self._ctrl_ref, self._cb_ref, C.byref(v),
+                                                    None if integ is None else integ.data_ptr(), out.buf.data_ptr(),
+                                                    None, raw_stream(self.device)), "qt_compute_action_obs")
         del keep
         return out.view
 

@@ -17,6 +17,10 @@
 #   profile    rocprofv3 trace + PMC passes of the bench (scripts/profile_session.sh)
 #   profw      the same for the config-3/5 workloads (scripts/profile_workloads.sh)
 #   prof       rocprofv3 trace + PMC_SETS passes of PROF_CMD (scripts/prof.sh)
+#   riders     config 5's 8-GPU shards timed on one GPU (run_workload.py --shard r/8, RANKS, default 0-7)
+#              with stationary riders and without (QT_RIDERS=0), alternating ALT times; then the
+#              whole config both ways
+#   small      the fused rollout at small per-GPU batches (scripts/small_batch.py), with a kernel trace
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -46,6 +50,19 @@ for step in ${STEPS:-tests smoke bench}; do
     profile) TAG=${TAG:-run} timeout -k 10 900 bash scripts/profile_session.sh > $O/profile.log 2>&1 || fail profile $O/profile.log ;;
     profw) TAG=${TAG:-run} timeout -k 10 900 bash scripts/profile_workloads.sh > $O/profw.log 2>&1 || fail profw $O/profw.log ;;
     prof) TAG=${TAG:-run} timeout -k 10 900 bash scripts/prof.sh ${PROF_CMD} > $O/prof.log 2>&1 || fail prof $O/prof.log ;;
+    riders) for a in $(seq 1 ${ALT:-1}); do for r in ${RANKS:-0 1 2 3 4 5 6 7}; do for rd in 1 0; do
+              QT_RIDERS=$rd timeout -k 10 120 python -u scripts/run_workload.py --config 5 --shard $r/8 --repeat 10 \
+                >> $O/riders.jsonl 2>> $O/riders.err || fail riders $O/riders.err
+            done; done; done
+            for rd in 1 0; do
+              QT_RIDERS=$rd timeout -k 10 200 python -u scripts/run_workload.py --config 5 --repeat 10 \
+                >> $O/riders_full.jsonl 2>> $O/riders.err || fail riders $O/riders.err
+            done ;;
+    small) timeout -k 10 300 python -u scripts/small_batch.py > $O/small_batch.jsonl 2> $O/small.err || fail small $O/small.err
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/small_trace -o run -- \
+             python3 scripts/small_batch.py --reps 10 > $O/small_trace.log 2>&1 || fail small $O/small_trace.log
+           cp $(find $O/small_trace -name "*kernel_stats.csv" | head -1) $O/small_kernel_stats.csv
+           cp $(find $O/small_trace -name "*kernel_trace.csv" | head -1) $O/small_kernel_trace.csv ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "$step done"

@@ -143,3 +143,40 @@ def test_profile_readers_use_one_named_directory(tmp_path):
     assert bench.profiled_kernel(rel2, tag) is None
     assert bench.pmc_traffic(rel2, tag) == (None, None)
     assert bench.issued_fp64(rel2, tag) is None
+
+
+RUN_WORKLOAD = os.path.join(ROOT, "scripts", "run_workload.py")
+
+
+@pytest.mark.parametrize("config,world", [(5, 2), (4, 3)])
+def test_run_workload_launcher_check(config, world):
+    """scripts/run_workload.py under torch.distributed.run (the configs 4 / 5
+    multi-GPU driver), on CPU: every rank joins (gloo) and rank 0 reports
+    world_size_seen, the backend and each rank's shard of the config, which
+    tile the global range."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", RUN_WORKLOAD, "--config", str(config),
+           "--gpus", str(world), "--launcher-check"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["world_size_seen"] == world and line["backend"] == "gloo"
+    ranks = line["ranks"]
+    assert [x["rank"] for x in ranks] == list(range(world))
+    total = {4: 262144, 5: 1048576}[config]
+    assert ranks[0]["lo"] == 0 and ranks[-1]["hi"] == total
+    assert all(a["hi"] == b["lo"] for a, b in zip(ranks, ranks[1:]))
+
+
+def test_run_workload_refuses_world_mismatch():
+    env = _env()
+    env.update({"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    r = subprocess.run([sys.executable, RUN_WORKLOAD, "--config", "5", "--gpus", "8", "--launcher-check"],
+                       capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr

@@ -665,6 +665,45 @@ def test_general_dare_random_systems(qt):
         np.testing.assert_allclose(K, np.linalg.solve(R + BtP @ B, BtP @ A), rtol=1e-9, atol=1e-12)
 
 
+def test_dense_dare_small_first_change_not_stopped_early(qt):
+    """the dense SDA's quadratic-regime early stop compares this
+    doubling's change with the last one's; before the first doubling there
+    is no last one.  A = diag(1e-5, 1), Q = diag(1, 1e-9): the first
+    doubling changes H by ~1e-9 of |H| (rel ~1e-18), but the marginal mode's
+    P[1][1] still has to grow from 1e-9 to 3.16e-5 at a linear rate.
+    Stopping after that first doubling (the old INFINITY start) returned
+    P[1][1] = 2e-9 and a gain 15,000x too small; the solution must be scipy's."""
+    import scipy.linalg as sl
+
+    from quadtrack import core, solve_dare
+
+    A = np.diag([1e-5, 1.0])
+    B = np.array([[0.0], [1.0]])
+    Q = np.diag([1.0, 1e-9])
+    R = np.eye(1)
+    Pref = sl.solve_discrete_are(A, B, Q, R)
+    Kref = np.linalg.solve(R + B.T @ Pref @ B, B.T @ Pref @ A)
+    P, K = solve_dare(A, B, Q, R)
+    np.testing.assert_allclose(P, Pref, rtol=1e-9, atol=1e-14)
+    np.testing.assert_allclose(K, Kref, rtol=1e-9, atol=1e-14)
+    # batched, beside well-conditioned problems in the same wavefront
+    m, dev = 8, torch.device("cuda:0")
+    As = np.stack([A if i % 2 == 0 else 0.5 * np.eye(2) for i in range(m)])
+    Bs, Qs, Rs = np.stack([B] * m), np.stack([Q if i % 2 == 0 else np.eye(2) for i in range(m)]), np.stack([R] * m)
+
+    def soa(x):
+        return torch.as_tensor(np.ascontiguousarray(x.reshape(m, -1).T), device=dev)
+
+    Kb, Pb, st, it = core.dare_dense(soa(As), soa(Bs), soa(Qs), soa(Rs), ab_per_problem=True)
+    assert st.cpu().tolist() == [0] * m
+    Kb = Kb.cpu().numpy().T.reshape(m, 1, 2)
+    Pb = Pb.cpu().numpy().T.reshape(m, 2, 2)
+    for i in range(0, m, 2):
+        np.testing.assert_allclose(Pb[i], Pref, rtol=1e-9, atol=1e-14)
+        np.testing.assert_allclose(Kb[i], Kref, rtol=1e-9, atol=1e-14)
+    assert int(it.max()) > 1
+
+
 @pytest.mark.parametrize("n,p", [(1, 1), (3, 8), (16, 1), (16, 8), (10, 6)])
 def test_dense_dare_batch_edge_sizes(qt, n, p):
     """The dense row kernel at its size limits (n <= 16, p <= 8, every

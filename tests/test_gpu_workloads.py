@@ -80,7 +80,10 @@ def _oracle_shard(config, lo, hi, idx=None):
     return met, xf, mass
 
 
-@pytest.mark.parametrize("config,lo,n", [(3, 40000, 384), (4, 200001, 384), (5, 777777, 640)])
+# (5, 777777, 700): 140 episodes per motion, so the grouped launch's
+# stationary riders fill the other groups' last waves (core.grouped_waves:
+# 12 waves, 15 without riders) and rider episodes are in the oracle sample
+@pytest.mark.parametrize("config,lo,n", [(3, 40000, 384), (4, 200001, 384), (5, 777777, 640), (5, 777777, 700)])
 def test_workload_sample_vs_oracle(qt, config, lo, n):
     from quadtrack import workloads
     from quadtrack.rollout import run_closed_loop
@@ -152,8 +155,73 @@ def test_workload_full_size_and_shard_independence(qt, config):
         sh = workloads.build(config, lo, hi)
         part = run_closed_loop(sh.controller, **sh.run_kwargs())
         assert torch.equal(part.metrics, met[:, lo:hi])
+    if config == 5:
+        # the 8-GPU layout: every rank's 131,072-episode shard is 2,048 whole
+        # waves (stationary riders in the other groups' last waves; 2,050
+        # without), and its results are still the full run's bit for bit
+        from quadtrack import core
+
+        for r in (0, 3, 7):
+            lo, hi = workloads.shard_bounds(total, r, 8)
+            sh = workloads.build(config, lo, hi)
+            part = run_closed_loop(sh.controller, **sh.run_kwargs())
+            assert core.launch_waves(part.batch) == 2048
+            assert core.grouped_waves(*part.batch.groups, riders=False) == 2050
+            assert torch.equal(part.metrics, met[:, lo:hi])
     del res, full
     torch.cuda.empty_cache()
+
+
+def test_riders_bitwise_and_deferred(qt, monkeypatch):
+    """Stationary riders (qt_rollout_grouped's one-launch layout): a mixed
+    batch run with riders equals the same batch with QT_RIDERS=0 bit for bit
+    (a rider runs its group's loop with the stationary target selected per
+    lane: the stationary loop's numbers), with fewer waves.  Then a rider
+    and a host lane of the same wave, and a stationary episode in its own
+    group, start outside the fast preconditions (roll beyond the tilt clamp):
+    their waves go to the exact pass, which runs each episode with its own
+    motion; the results match the exact step everywhere (recording) to 1e-9."""
+    from quadtrack import core
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import build_batch, run_closed_loop
+
+    n = 1100  # 220 per motion: each group's last wave has 36 free lanes
+    motion = [i % 5 for i in range(n)]
+    ctl = BatchedRiccatiLQR({"dt": 0.01})
+    runs = {}
+    for riders in ("1", "0"):
+        monkeypatch.setenv("QT_RIDERS", riders)
+        runs[riders] = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=600)
+    g = runs["1"].batch.groups
+    assert core.grouped_waves(*g, riders=True) == 18 and core.grouped_waves(*g, riders=False) == 20
+    assert torch.equal(runs["1"].metrics, runs["0"].metrics)
+    assert torch.equal(runs["1"].state.x, runs["0"].state.x)
+    assert torch.equal(runs["1"].state.target, runs["0"].state.target)
+
+    monkeypatch.setenv("QT_RIDERS", "1")
+    from quadtrack.env.config import EnvConfig
+
+    env = EnvConfig.from_dict({}).to_params()
+    crit = core.criteria()
+    out = []
+    for record in (False, True):
+        batch, perm = build_batch(ctl, {}, n, seeds=np.arange(n), motion=motion).physical_groups()
+        st = core.RolloutState.empty(n, batch.device)
+        core.reset(env, batch, st)
+        # slots in group order sinusoidal, figure-8, circular, linear,
+        # stationary (220 each): slot 880 rides in the sinusoidal group's last
+        # wave (slots 192..219 + riders), slot 200 is a host lane of that wave,
+        # slot 1090 a stationary episode in the stationary group's own waves
+        for slot in (880, 200, 1090):
+            st.x[6, slot] = 1.2
+        for k in (150, 450):
+            rec = torch.full((k, 16, n), float("nan"), dtype=torch.float64, device=batch.device) if record else None
+            core.rollout(env, ctl.ctrl, crit, batch, st, k, rec)
+        out.append((core.episode_metrics(crit, st).cpu().numpy(), st.x.cpu().numpy()))
+    (mf, xf), (me, xe) = out
+    np.testing.assert_array_equal(mf[O.MET_FIELDS.index("steps")], me[O.MET_FIELDS.index("steps")])
+    np.testing.assert_allclose(mf, me, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(xf, xe, rtol=1e-9, atol=1e-9)
 
 
 @pytest.mark.parametrize("horizon", [450, 3000])

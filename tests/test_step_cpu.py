@@ -137,3 +137,49 @@ def test_action_tensor_forms():
     np.testing.assert_array_equal(action_tensor(np.ones((3, 4)), 3, dev).numpy(), np.ones((3, 4)))
     with pytest.raises(ValueError, match="shape"):
         action_tensor(np.ones((3, 3)), 3, dev)
+
+
+def test_frame_pool_without_the_storage_use_count(monkeypatch):
+    """A torch build without the private torch._C._storage_Use_Count: the
+    frame pool and the action buffers fall back to fresh allocations (never
+    recycled) instead of failing, and every handed-out view still works."""
+    import quadtrack.step as S
+
+    monkeypatch.setattr(S, "_CAN_RECYCLE", False)
+    monkeypatch.delattr(torch._C, "_storage_Use_Count")
+    pool = FramePool(4, torch.device("cpu"), size=3)
+    cur, seen = None, []
+    for k in range(5):
+        fr = pool.take(cur)
+        fr.f.fill_(float(k))
+        obs, rew, done, info = fr.seal().step_result(with_action=True)
+        assert not fr.recyclable()
+        assert torch.equal(obs["quadcopter"]["position"], torch.full((4, 3), float(k), dtype=torch.float64))
+        cur = fr
+        seen.append(fr)
+        del fr, obs, rew, done, info
+    assert len({id(f) for f in seen}) == 5  # a new frame every step
+    # what an earlier step handed out keeps its values
+    for k, f in enumerate(seen):
+        assert torch.equal(f.f, torch.full_like(f.f, float(k)))
+    o = _Out(4, 3, torch.device("cpu"))
+    assert not o.free()
+
+
+def test_dlpack_export_keeps_the_frame():
+    """A DLPack capsule (or a numpy array) of an observation tensor holds the
+    frame's storage: the frame is not recycled while the export lives, even
+    after the Python view itself is dropped."""
+    from torch.utils.dlpack import to_dlpack
+
+    fr = Frame(6, torch.device("cpu")).seal()
+    obs = fr.observation()
+    cap = to_dlpack(obs["quadcopter"]["velocity"])
+    del obs
+    assert not fr.recyclable()
+    del cap
+    assert fr.recyclable()
+    arr = fr.step_result()[1].numpy()
+    assert not fr.recyclable()
+    del arr
+    assert fr.recyclable()

@@ -61,6 +61,39 @@ def test_motion_groups_layout(counts):
     assert np.array_equal(to.numpy(), order) and tsm == sm and tse == se
 
 
+def test_grouped_waves_with_stationary_riders(monkeypatch):
+    """core.grouped_waves (qt_rollout.hip grouped_waves): stationary riders
+    fill every other group's last wave, so a batch needs ceil(n / 64) waves
+    when the stationary group can cover the gaps — config 5's 8-GPU shards
+    2,048 (2,050 without riders), the whole config 16,384 (16,385) — and no
+    fewer than the groups' own waves otherwise.  QT_RIDERS=0 turns them off."""
+    import numpy as np
+
+    from quadtrack import workloads
+
+    def waves(lo, hi, riders=None):
+        _, sm, se = core.motion_groups(workloads.motion_of(lo, hi))
+        return core.grouped_waves(sm, se, riders)
+
+    for r in range(8):
+        lo, hi = workloads.shard_bounds(1048576, r, 8)
+        assert (waves(lo, hi, True), waves(lo, hi, False)) == (2048, 2050)
+    assert (waves(0, 1048576, True), waves(0, 1048576, False)) == (16384, 16385)
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        counts = rng.integers(0, 300, size=5)
+        sm = [k for k in core.group_order() if counts[k]]
+        se = list(np.cumsum([counts[k] for k in sm]))
+        own = sum(-(-int(counts[k]) // 64) for k in sm)
+        gaps = sum((-int(counts[k])) % 64 for k in sm if k != 0)
+        w = core.grouped_waves(sm, se, True)
+        assert w >= -(-int(counts.sum()) // 64) and w <= own
+        if counts[0] >= gaps:
+            assert w == -(-int(counts.sum()) // 64)
+    monkeypatch.setenv("QT_RIDERS", "0")
+    assert core.grouped_waves(*core.motion_groups(workloads.motion_of(0, 131072))[1:]) == 2050
+
+
 def test_group_order_knob_is_validated_when_used(monkeypatch):
     """QT_GROUP_ORDER (an A/B knob) is read when a grouping is made: a
     malformed value raises there with the variable named, and never breaks
