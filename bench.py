@@ -16,8 +16,9 @@ launches (partials, + one async RCCL all-reduce of the sums when N > 1).
 value = all ranks' env-steps / max-over-ranks wall time.
 
 Beside it (rank 0, N = 1, untimed for `value`): the per-step API leg
-(`step_api`: 1,048,576 episodes stepped one launch per step from Python by
-BatchedQuadcopterEnv.step_closed, the state round-tripping HBM each step;
+(`step_api`: 4,194,304 episodes stepped one launch per step from Python by
+BatchedQuadcopterEnv.step_closed, the state round-tripping HBM each step —
+~1.9 GB per step, far beyond the 256 MB Infinity Cache, so the rate is HBM's;
 GB/s against the 8 TB/s HBM peak), the DARE throughput and the CPU baseline.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -73,7 +74,7 @@ def parse():
     ap.add_argument("--cpu-sample-1core", type=int, default=4096, help="episodes of the 1-thread CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the OpenMP CPU leg (0: see cpu_baseline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--step-api-episodes", type=int, default=1048576,
+    ap.add_argument("--step-api-episodes", type=int, default=4194304,
                     help="episodes of the per-step API leg (rank 0, N=1; 0 skips it)")
     ap.add_argument("--step-api-steps", type=int, default=100)
     ap.add_argument("--profile-dir", default=PROFILE_DIR,

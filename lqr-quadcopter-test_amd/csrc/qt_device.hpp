@@ -354,7 +354,7 @@ __device__ __forceinline__ void trig_of(const double* ang, Trig& t) {
 // has |delta| <= kRateAngle and takes the shorter rate_sincos.
 template <bool SMALL = false, bool YAW0 = false>
 __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, const double* delta, Trig& t,
-                                           const RateCoef& rk = RateCoef{}) {
+                                           const RateCoef& rk = RateCoef{}, const SmallCoef& sk = SmallCoef{}) {
   constexpr int NA = YAW0 ? 2 : 3;
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -362,7 +362,7 @@ __device__ __forceinline__ void trig_shift(const double* ang, const Trig& t0, co
     if (YAW0)
       rate_sincos(delta[i], &sd, &cd, rk);
     else
-      small_sincos(delta[i], &sd, &cd);
+      small_sincos(delta[i], &sd, &cd, sk);
     t.s[i] = fma(t0.s[i], cd, t0.c[i] * sd);
     t.c[i] = fma(t0.c[i], cd, -(t0.s[i] * sd));
   }
@@ -738,7 +738,7 @@ __device__ __forceinline__ void integrate_yaw0(const RateLin& R, const VelLin& L
 template <int INTEG = -1>
 __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const RateLin& R, const VelLin& L,
                                                  const Plant& pl, const Trig& ta, double* x, const double* u,
-                                                 double* d4, Trig& t4) {
+                                                 double* d4, Trig& t4, const SmallCoef& sk = SmallCoef{}) {
   const double w[3] = {x[9], x[10], x[11]};
   double d2[3], d3[3];
 #pragma unroll
@@ -749,17 +749,19 @@ __device__ __forceinline__ void integrate_closed(const qt_env_params& e, const R
   }
   Trig t[4];
   t[0] = ta;
-  trig_shift<true>(x + 6, ta, d4, t[3]);
+  trig_shift<true>(x + 6, ta, d4, t[3], RateCoef{}, sk);
   double em = 0.0;
   if (INTEG == 0 || (INTEG < 0 && e.integrator != 1)) {
-    trig_shift<true>(x + 6, ta, d2, t[1]);
+    trig_shift<true>(x + 6, ta, d2, t[1], RateCoef{}, sk);
     // the third stage from the second by e3 = d3 - d2 = O(dt^2) (resid_sincos)
+    RateCoef rk;
+    rk.s5 = sk.s5;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const double e3 = fma(R.e3y, w[i], R.d3u * u[1 + i]);
       em = fmax(em, fabs(e3));
       double sd, cm;
-      resid_sincos(e3, &sd, &cm);
+      resid_sincos(e3, &sd, &cm, rk);
       rotate_cm(t[1].s[i], t[1].c[i], sd, cm, &t[2].s[i], &t[2].c[i]);
     }
   }
@@ -880,7 +882,7 @@ __device__ __forceinline__ void integrate(const qt_env_params& e, const Plant& p
 // evaluates with a drift of a few ulp per step (as the fast step's,
 // attitude_trig_resid); a launch starts from the direct evaluation.
 __device__ __forceinline__ void carry_attitude_trig(const double* a0, const double* a1, const double* d4,
-                                                    const Trig& t4, Trig& ta) {
+                                                    const Trig& t4, Trig& ta, const SmallCoef& sk = SmallCoef{}) {
   bool far[3], any = false;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -888,7 +890,7 @@ __device__ __forceinline__ void carry_attitude_trig(const double* a0, const doub
     far[i] = !(fabs(r) <= kAdvanceAngle);
     any = any | far[i];
     double sd, cm;
-    tiny_sincos(r, &sd, &cm);
+    tiny_sincos(r, &sd, &cm, sk);
     rotate_cm(t4.s[i], t4.c[i], sd, cm, &ta.s[i], &ta.c[i]);
   }
   if (any_lane(any)) {

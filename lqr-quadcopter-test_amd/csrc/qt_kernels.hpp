@@ -277,17 +277,57 @@ __device__ __forceinline__ double sq3_ref(double a, double b, double c) {
   return (a * a + b * b) + c * c;
 }
 
+// A loop-invariant uniform value held in a VGPR pair (every lane a copy).
+// The inline asm's VGPR result is divergent to the compiler, so the value
+// takes no SGPR and is never rematerialised: for a loop whose uniform values
+// overflow the wave's 102 SGPRs, which the compiler otherwise spills to VGPR
+// lanes and reads back with v_readlane in every step (the exact step).
+__device__ __forceinline__ double vpin(double x) {
+  double r;
+  asm("v_mov_b64 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// QT_EXACT_VPIN bits: 1 the env / controller / plant uniforms, 2 the
+// closed-form rate and velocity maps, 4 the Taylor coefficients (SmallCoef),
+// 8 the gains
+#ifndef QT_EXACT_VPIN
+#define QT_EXACT_VPIN 5
+#endif
+
 // The closed-loop steps of one lane.  FAST: the branch-light step of
 // qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
 // takes the exact step's decisions; rare lanes/steps (speed at the
 // clamp, attitude far outside [-pi, pi), tracking error at the radius within
 // 1e-14) fall back to the exact constraint / comparison code inside the step.
 template <bool FAST, int MOTION, int KC, bool FF, bool KS, int INTEG = -1>
-__device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
-                                          int motion, const Pattern& pt, const Plant& pl, double hover,
-                                          const Gains<KC, KS>& G, const FFLane& fl, double* x, double* integ,
+__device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl_params& c0, const qt_criteria& cr,
+                                          int motion, const Pattern& pt, const Plant& pl0, double hover,
+                                          const Gains<KC, KS>& G0, const FFLane& fl, double* x, double* integ,
                                           Target& tg, double& t, Acc& a, int nsteps, double* __restrict__ rec,
                                           int64_t n, int64_t ep, double* __restrict__ reward = nullptr) {
+  // the exact step: its loop-invariant uniforms (env limits, controller
+  // clamps, gains, plant) held in VGPRs (vpin) instead of spilled SGPRs
+  constexpr bool kPin = !FAST && (QT_EXACT_VPIN & 1);
+  constexpr bool kPinLin = !FAST && (QT_EXACT_VPIN & 2);
+  constexpr bool kPinTaylor = !FAST && (QT_EXACT_VPIN & 4);
+  qt_env_params e = e0;
+  qt_ctrl_params c = c0;
+  Plant pl = pl0;
+  Gains<KC, KS> G = G0;
+  if (kPin) {
+    e.min_thrust = vpin(e.min_thrust), e.max_thrust = vpin(e.max_thrust);
+    e.max_angular_rate = vpin(e.max_angular_rate), e.dt = vpin(e.dt);
+    e.max_episode_time = vpin(e.max_episode_time), e.max_velocity = vpin(e.max_velocity);
+    e.max_angular_velocity = vpin(e.max_angular_velocity), e.max_position = vpin(e.max_position);
+    e.target_radius = vpin(e.target_radius);
+    for (int i = 0; i < 3; ++i) e.center[i] = vpin(e.center[i]);
+    c.min_thrust = vpin(c.min_thrust), c.max_thrust = vpin(c.max_thrust), c.max_rate = vpin(c.max_rate);
+    pl.inv_mass = vpin(pl.inv_mass), pl.gz = vpin(pl.gz);
+  }
+  if (!FAST && (QT_EXACT_VPIN & 8)) {
+    for (int j = 0; j < Gains<KC, KS>::kCount; ++j) G.k[j] = vpin(G.k[j]);
+  }
   const double R = cr.target_radius;
   const double er2lo = e.target_radius * e.target_radius * (1.0 - 1e-14);
   const double er2hi = e.target_radius * e.target_radius * (1.0 + 1e-14);
@@ -319,8 +359,18 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
   // full-gain fast step (kFast, whose launch knows the integrator is RK4)
   Trig ta;
   trig_of(x + 6, ta);
-  const RateLin rl = make_rate_lin(e);
-  const VelLin vl = make_vel_lin(e, pl);
+  RateLin rl = make_rate_lin(e);
+  VelLin vl = make_vel_lin(e, pl);
+  if (kPinLin) {
+    rl.wy = vpin(rl.wy), rl.wu = vpin(rl.wu), rl.ay = vpin(rl.ay), rl.au = vpin(rl.au), rl.h2 = vpin(rl.h2);
+    rl.d3y = vpin(rl.d3y), rl.d3u = vpin(rl.d3u), rl.d4y = vpin(rl.d4y), rl.d4u = vpin(rl.d4u);
+    rl.e3y = vpin(rl.e3y);
+    vl.cv = vpin(vl.cv), vl.pv = vpin(vl.pv), vl.gv = vpin(vl.gv), vl.gp = vpin(vl.gp);
+    for (int i = 0; i < 4; ++i) vl.wv[i] = vpin(vl.wv[i]);
+    for (int i = 0; i < 3; ++i) vl.pa[i] = vpin(vl.pa[i]);
+  }
+  SmallCoef sk;  // the stage / carry Taylor coefficients (pinned in VGPRs in the exact step)
+  if (kPinTaylor) sk.pin();
   for (int s = 0; s < nsteps; ++s) {
     if (a.term != QT_TERM_RUNNING) break;
     // ---- compute_action on the current observation (riccati_lqr.py:779-967)
@@ -398,10 +448,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e, const qt_ctrl_
       double ua[4], a0[3] = {x[6], x[7], x[8]}, d4[3];
       a.viol += parse_action(e, u, ua);
       Trig t4;
-      integrate_closed<INTEG>(e, rl, vl, pl, ta, x, ua, d4, t4);
+      integrate_closed<INTEG>(e, rl, vl, pl, ta, x, ua, d4, t4, sk);
       t += e.dt;
       const int term = constrain_terminate<false>(e, x, t);
-      carry_attitude_trig(a0, x + 6, d4, t4, ta);
+      carry_attitude_trig(a0, x + 6, d4, t4, ta, sk);
       if (!(QT_ABLATE & QT_ABL_TARGET)) target_state<FF>(e, motion, pt, t, tg);
       const double q0 = x[0] - tg.p[0], q1 = x[1] - tg.p[1], q2 = x[2] - tg.p[2];
       err_pre = sqrt_noscale(sq3_ref(q0, q1, q2));  // this step's post-step error, the next one's pre-step

@@ -68,17 +68,41 @@ QT_HD void fast_sincos(double x, double* s, double* c) {
 // at the default limits.
 constexpr double kSmallAngle = 0.125;
 
-QT_HD void small_sincos(double d, double* s, double* c) {
+// The Taylor coefficients of small_sincos, resid_sincos and tiny_sincos as
+// values (defaults: the literals, which the optimiser folds as before).  A
+// loop short of scalar registers (the exact step) pins them in vector
+// registers once (pin: no instruction emitted) instead of re-materialising
+// each 64-bit constant with two s_mov per use.
+struct SmallCoef {
+  double s9 = 2.7557319223985893e-06;   // 1/9!
+  double s7 = -1.9841269841269841e-04;  // -1/7!
+  double s5 = 8.3333333333333332e-03;   // 1/5!
+  double s3 = -1.6666666666666666e-01;  // -1/3!
+  double c10 = -2.7557319223985888e-07;  // -1/10!
+  double c8 = 2.4801587301587302e-05;   // 1/8!
+  double c6 = -1.3888888888888889e-03;  // -1/6!
+  double c4 = 4.1666666666666664e-02;   // 1/4!
+  double third = 3.3333333333333331e-01;  // tiny_sincos' 1/3
+#if defined(__HIP_DEVICE_COMPILE__)
+  __device__ __forceinline__ void pin() {
+    asm("" : "+v"(s9), "+v"(s7), "+v"(s5), "+v"(s3), "+v"(c10), "+v"(c8), "+v"(c6), "+v"(c4), "+v"(third));
+  }
+#else
+  void pin() {}
+#endif
+};
+
+QT_HD void small_sincos(double d, double* s, double* c, const SmallCoef& k = SmallCoef{}) {
   const double z = d * d;
-  double p = 2.7557319223985893e-06;  // 1/9!
-  p = fma(z, p, -1.9841269841269841e-04);  // -1/7!
-  p = fma(z, p, 8.3333333333333332e-03);  // 1/5!
-  p = fma(z, p, -1.6666666666666666e-01);  // -1/3!
+  double p = k.s9;  // 1/9!
+  p = fma(z, p, k.s7);  // -1/7!
+  p = fma(z, p, k.s5);  // 1/5!
+  p = fma(z, p, k.s3);  // -1/3!
   *s = fma(d * z, p, d);
-  double q = -2.7557319223985888e-07;  // -1/10!
-  q = fma(z, q, 2.4801587301587302e-05);  // 1/8!
-  q = fma(z, q, -1.3888888888888889e-03);  // -1/6!
-  q = fma(z, q, 4.1666666666666664e-02);  // 1/4!
+  double q = k.c10;  // -1/10!
+  q = fma(z, q, k.c8);  // 1/8!
+  q = fma(z, q, k.c6);  // -1/6!
+  q = fma(z, q, k.c4);  // 1/4!
   q = fma(z, q, -0.5);
   *c = fma(z, q, 1.0);
 }
@@ -163,9 +187,9 @@ QT_HD void resid_sincos(double d, double* s, double* cm, const RateCoef& k = Rat
 // -d^2 / 2, truncation below 3e-22 (sin) and 4.2e-18 (cos - 1).
 constexpr double kAdvanceAngle = 1e-4;
 
-QT_HD void tiny_sincos(double d, double* s, double* cm) {
+QT_HD void tiny_sincos(double d, double* s, double* cm, const SmallCoef& k = SmallCoef{}) {
   *cm = d * (-0.5 * d);
-  *s = fma(d * *cm, 3.3333333333333331e-01, d);  // d + d (-d^2 / 2) / 3
+  *s = fma(d * *cm, k.third, d);  // d + d (-d^2 / 2) / 3
 }
 
 // (s, c) rotated by the angle whose sine is sd and cosine 1 + cm:

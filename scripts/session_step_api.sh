@@ -4,8 +4,8 @@
 # steps:
 #   tests  pytest of the per-step API (tests/test_gpu_batched_env.py; PYTEST_ARGS adds)
 #   bench  scripts/step_api_bench.py at 65,536 and 1,048,576 episodes, both modes, LQR and LQI
-#   trace  rocprofv3 kernel trace + stats of the bench loop (1,048,576 and 65,536 episodes, 3,000 steps)
-#   pmc    FETCH_SIZE and WRITE_SIZE passes of the same loop (1,048,576 and 65,536 episodes, 300 steps)
+#   trace  rocprofv3 kernel trace + stats of the bench loop (NS episodes, default 1,048,576 and 65,536; 3,000 steps)
+#   pmc    FETCH_SIZE and WRITE_SIZE passes of the same loop (NS episodes, 300 steps)
 #   sq     SQ and F64 passes of the closed step at 1,048,576 episodes (VALU / FP64 issue beside HBM)
 #   exact  the exact step at 65,536 linear LQR episodes (scripts/flavour_timing.py --cases exact):
 #          timing, kernel trace, SQ / SQ2 / F64 passes
@@ -25,15 +25,15 @@ for step in ${STEPS:-tests bench}; do
     tests) timeout -k 10 900 python -u -m pytest tests/test_gpu_batched_env.py -x -v --timeout 300 --timeout-method thread \
              ${PYTEST_ARGS:-} > $O/tests.log 2>&1 || fail tests $O/tests.log
            tail -3 $O/tests.log ;;
-    bench) timeout -k 10 600 python -u $LOOP --n 65536 1048576 --steps 3000 > $O/step_api.jsonl 2> $O/bench.err \
+    bench) timeout -k 10 600 python -u $LOOP --n ${NS:-65536 1048576} --steps 3000 > $O/step_api.jsonl 2> $O/bench.err \
              || fail bench $O/bench.err
            cat $O/step_api.jsonl ;;
-    trace) for n in 1048576 65536; do
+    trace) for n in ${NS:-1048576 65536}; do
              timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$n -o run -- \
                python3 $LOOP --n $n --steps 3000 --warm 20 > $O/trace_$n.log 2>&1 || fail trace $O/trace_$n.log
              cp $(find $O/trace_$n -name "*kernel_stats.csv" | head -1) $O/step_api_kernel_stats_$n.csv
            done ;;
-    pmc) for n in 1048576 65536; do
+    pmc) for n in ${NS:-1048576 65536}; do
            for P in FETCH_SIZE WRITE_SIZE; do
              timeout -k 10 -s KILL 300 rocprofv3 --pmc $P --output-format csv -d $O/pmc_${P}_$n -o run -- \
                python3 $LOOP --n $n --steps 300 --warm 5 > $O/pmc_${P}_$n.log 2>&1 || fail pmc $O/pmc_${P}_$n.log
