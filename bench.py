@@ -439,6 +439,17 @@ def step_api_leg(args, cfg, dev):
     host_s = time.perf_counter() - t0
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / k
+    # what the timed loop computed: the first 1,024 episodes' state after its
+    # 10 + k steps against the fused rollout of the same episodes for as many
+    # steps (another kernel: the closed-form fast step, not the staged exact
+    # step the per-step API runs)
+    from quadtrack.rollout import run_closed_loop
+
+    m = min(n, 1024)
+    ref = run_closed_loop(BatchedRiccatiLQR({"dt": 0.01}, device=dev), cfg, n=m, seeds=np.arange(m),
+                          max_steps=10 + k)
+    got = env.frame.f[0:12, :m]
+    check = float((got - ref.state.x).abs().max().item())
     gbps = STEP_API_BYTES * n / (ms * 1e-3) / 1e9
     out = {"episodes": n, "steps": k, "launches_per_step": 1, "ms_per_step": round(ms, 5),
            "env_steps_per_s": round(n / (ms * 1e-3), 1), "host_us_per_step": round(host_s / k * 1e6, 2),
@@ -448,7 +459,8 @@ def step_api_leg(args, cfg, dev):
            # env-steps/s x 200 B / peak; the frame moves the observation and info besides
            "survey_bytes_per_env_step": SURVEY_STEP_BYTES,
            "survey_hbm_frac": round(SURVEY_STEP_BYTES * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "kernel": "closed_step_kernel<6, no-FF, structured K, freeze> (qt_frame_closed_step)"}
+           "kernel": "closed_step_kernel<6, no-FF, structured K, freeze> (qt_frame_closed_step)",
+           "check_vs_fused_max_abs_diff": check, "check_episodes": m}
     del env, ctl
     torch.cuda.empty_cache()
     return out

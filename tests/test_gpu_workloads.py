@@ -172,6 +172,44 @@ def test_workload_full_size_and_shard_independence(qt, config):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("case", ["lqi", "pid", "feedforward", "mass"])
+def test_riders_bitwise_other_loops(qt, monkeypatch, case):
+    """Stationary riders in the other controllers' and options' loops: LQI
+    (9-column gains, folded target rotor), PID (3 gains, observation time),
+    feed-forward (the target acceleration a rider must see as zero) and
+    per-episode plant mass with per-episode gains (config 5's form).  With
+    riders and without (QT_RIDERS=0) bit for bit: metrics, state, target
+    observation and controller integral."""
+    from quadtrack.controllers import BatchedPID, BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    n = 1100
+    motion = [i % 5 for i in range(n)]
+    mass = None
+    if case == "lqi":
+        ctl = BatchedRiccatiLQR({"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2],
+                                 "integral_limit": 10.0, "integral_zero_threshold": 0.01})
+    elif case == "pid":
+        ctl = BatchedPID({})
+    elif case == "feedforward":
+        ctl = BatchedRiccatiLQR({"dt": 0.01, "feedforward_enabled": True, "ff_velocity_gain": 0.5,
+                                 "ff_acceleration_gain": 0.2})
+    else:
+        mass = 0.8 + 0.4 * np.random.default_rng(5).random(n)
+        ctl = BatchedRiccatiLQR({"dt": 0.01}, mass=mass)
+    runs = {}
+    for riders in ("1", "0"):
+        monkeypatch.setenv("QT_RIDERS", riders)
+        runs[riders] = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, plant_mass=mass,
+                                       max_steps=700)
+    a, b = runs["1"], runs["0"]
+    assert a.batch.groups is not None
+    assert torch.equal(a.metrics, b.metrics)
+    assert torch.equal(a.state.x, b.state.x)
+    assert torch.equal(a.state.target, b.state.target)
+    assert torch.equal(a.state.integ, b.state.integ)
+
+
 def test_riders_bitwise_and_deferred(qt, monkeypatch):
     """Stationary riders (qt_rollout_grouped's one-launch layout): a mixed
     batch run with riders equals the same batch with QT_RIDERS=0 bit for bit
