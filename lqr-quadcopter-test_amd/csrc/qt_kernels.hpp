@@ -294,6 +294,10 @@ __device__ __forceinline__ double vpin(double x) {
 #ifndef QT_EXACT_VPIN
 #define QT_EXACT_VPIN 5
 #endif
+// the same for the full-gain fast step (kFast's run_steps<true>)
+#ifndef QT_FAST_VPIN
+#define QT_FAST_VPIN 0
+#endif
 
 // The closed-loop steps of one lane.  FAST: the branch-light step of
 // qt_device.hpp (fast_path_ok + finite lane inputs, no recording), which
@@ -308,9 +312,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
                                           int64_t n, int64_t ep, double* __restrict__ reward = nullptr) {
   // the exact step: its loop-invariant uniforms (env limits, controller
   // clamps, gains, plant) held in VGPRs (vpin) instead of spilled SGPRs
-  constexpr bool kPin = !FAST && (QT_EXACT_VPIN & 1);
-  constexpr bool kPinLin = !FAST && (QT_EXACT_VPIN & 2);
-  constexpr bool kPinTaylor = !FAST && (QT_EXACT_VPIN & 4);
+  constexpr int kPinBits = FAST ? QT_FAST_VPIN : QT_EXACT_VPIN;
+  constexpr bool kPin = kPinBits & 1;
+  constexpr bool kPinLin = kPinBits & 2;
+  constexpr bool kPinTaylor = kPinBits & 4;
   qt_env_params e = e0;
   qt_ctrl_params c = c0;
   Plant pl = pl0;
@@ -325,7 +330,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
     c.min_thrust = vpin(c.min_thrust), c.max_thrust = vpin(c.max_thrust), c.max_rate = vpin(c.max_rate);
     pl.inv_mass = vpin(pl.inv_mass), pl.gz = vpin(pl.gz);
   }
-  if (!FAST && (QT_EXACT_VPIN & 8)) {
+  if (kPinBits & 8) {
     for (int j = 0; j < Gains<KC, KS>::kCount; ++j) G.k[j] = vpin(G.k[j]);
   }
   const double R = cr.target_radius;
@@ -414,7 +419,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
       // the command is finite and inside the env clamps: parsing is the identity
       double a0[3] = {x[6], x[7], x[8]}, d4[3];
       Trig t4;
-      integrate_closed<0>(e, rl, vl, pl, ta, x, u, d4, t4);
+      integrate_closed<0>(e, rl, vl, pl, ta, x, u, d4, t4, sk);
       t += e.dt;
       if (!(QT_ABLATE & QT_ABL_TARGET)) {
         if constexpr (kCarry)
@@ -438,7 +443,7 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
         if (!(QT_ABLATE & QT_ABL_CONSTRAIN)) constrain<false>(e, x);
         a.on_post += norm_le(se, e.target_radius);
       }
-      carry_attitude_trig(a0, x + 6, d4, t4, ta);
+      carry_attitude_trig(a0, x + 6, d4, t4, ta, sk);
       if (QT_ABLATE & QT_ABL_TERMINATION)
         a.term = t >= e.max_episode_time ? QT_TERM_TIME_LIMIT : QT_TERM_RUNNING;
       else
