@@ -304,7 +304,7 @@ __device__ __forceinline__ double vpin(double x) {
 // takes the exact step's decisions; rare lanes/steps (speed at the
 // clamp, attitude far outside [-pi, pi), tracking error at the radius within
 // 1e-14) fall back to the exact constraint / comparison code inside the step.
-template <bool FAST, int MOTION, int KC, bool FF, bool KS, int INTEG = -1>
+template <bool FAST, int MOTION, int KC, bool FF, bool KS, int INTEG = -1, bool PIN = true>
 __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl_params& c0, const qt_criteria& cr,
                                           int motion, const Pattern& pt, const Plant& pl0, double hover,
                                           const Gains<KC, KS>& G0, const FFLane& fl, double* x, double* integ,
@@ -312,7 +312,10 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
                                           int64_t n, int64_t ep, double* __restrict__ reward = nullptr) {
   // the exact step: its loop-invariant uniforms (env limits, controller
   // clamps, gains, plant) held in VGPRs (vpin) instead of spilled SGPRs
-  constexpr int kPinBits = FAST ? QT_FAST_VPIN : QT_EXACT_VPIN;
+  // PIN (the exact kernel's launch choice, ExactLaunch): off for batches of
+  // more than one wave per SIMD, where a second resident wave (unpinned: <=
+  // 256 VGPRs) hides the FP64 latency that pinning's fewer instructions cannot
+  constexpr int kPinBits = FAST ? QT_FAST_VPIN : (PIN ? QT_EXACT_VPIN : 0);
   constexpr bool kPin = kPinBits & 1;
   constexpr bool kPinLin = kPinBits & 2;
   constexpr bool kPinTaylor = kPinBits & 4;
@@ -954,7 +957,7 @@ __device__ __forceinline__ void run_yaw0(const qt_env_params& e, const qt_ctrl_p
 // (lc.reward); without them the exact loop carries neither pointer.  INTEG
 // (the exact flavour): the integrator, known at launch (integrate_closed).
 template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool FRESH = true, bool REC = true,
-          int INTEG = -1, bool RIDE = false>
+          int INTEG = -1, bool RIDE = false, bool PIN = true>
 __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                              const BatchDev& b, const qt_state& st, int nsteps,
                                              double* __restrict__ rec, int deferred, const LaunchConst& lc,
@@ -1097,7 +1100,7 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
     }
   } else {
     if (deferred != kExact && wave_ok) return;
-    run_steps<false, MOTION, KC, FF, KS, INTEG>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
+    run_steps<false, MOTION, KC, FF, KS, INTEG, PIN>(e, c, cr, motion, pt, pl, hover, G, fl, x, integ, tg, t, a, nsteps,
                                          REC ? rec : nullptr, n, ep, REC ? lc.reward : nullptr);
   }
   // Without feed-forward the loop leaves the acceleration rows at zero (only
@@ -1114,7 +1117,8 @@ __device__ __forceinline__ void rollout_lane(const qt_env_params& e, const qt_ct
   if (FRESH && lc.met) store_metrics(cr, a, t, lc.met, n, ep);  // a fresh pass: the metrics rows (metrics_kernel)
 }
 
-template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool REC = true, int INTEG = -1>
+template <int FLAVOR, int MOTION, int KC, bool FF, bool KS, bool UNI = false, bool REC = true, int INTEG = -1,
+          bool PIN = true>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                          BatchDev b, qt_state st, int nsteps,
                                                          double* __restrict__ rec, int deferred, LaunchConst lc) {
@@ -1123,7 +1127,8 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(qt_env_params e, qt_ctr
   if (FLAVOR == kExact && deferred != kExact && lc.defer_flag && *lc.defer_flag != lc.epoch) return;
   const int64_t slot = slot_at(b, (int64_t)blockIdx.x * kBlock + threadIdx.x);
   if (slot < 0) return;
-  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI, true, REC, INTEG>(e, c, cr, b, st, nsteps, rec, deferred, lc, slot);
+  rollout_lane<FLAVOR, MOTION, KC, FF, KS, UNI, true, REC, INTEG, false, PIN>(e, c, cr, b, st, nsteps, rec, deferred, lc,
+                                                                             slot);
 }
 
 // The yaw-at-rest fast flavour over a batch grouped by motion type

@@ -561,12 +561,39 @@ struct ExactLaunch {
   static void launch(int deferred, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                      const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, double* rec,
                      const LaunchConst& lc) {
-    if (rec || lc.reward)
-      rollout_kernel<kExact, MOTION, KC, FF, KS, false, true, INTEG><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
-                                                                                          rec, deferred, lc);
-    else  // no recording, no rewards: the loop without either pointer
-      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false, INTEG><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps,
-                                                                                           nullptr, deferred, lc);
+    // uniforms pinned in VGPRs (run_steps' PIN) while the launch holds at
+    // most one wave per SIMD; a bigger one keeps two waves per SIMD resident
+    const bool pin = (int64_t)grid * kBlock <= pin_lanes();
+    if (rec || lc.reward) {
+      if (pin)
+        rollout_kernel<kExact, MOTION, KC, FF, KS, false, true, INTEG, true><<<grid, kBlock, 0, s>>>(
+            e, c, cr, b, st, nsteps, rec, deferred, lc);
+      else
+        rollout_kernel<kExact, MOTION, KC, FF, KS, false, true, INTEG, false><<<grid, kBlock, 0, s>>>(
+            e, c, cr, b, st, nsteps, rec, deferred, lc);
+    } else if (pin) {  // no recording, no rewards: the loop without either pointer
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false, INTEG, true><<<grid, kBlock, 0, s>>>(
+          e, c, cr, b, st, nsteps, nullptr, deferred, lc);
+    } else {
+      rollout_kernel<kExact, MOTION, KC, FF, KS, false, false, INTEG, false><<<grid, kBlock, 0, s>>>(
+          e, c, cr, b, st, nsteps, nullptr, deferred, lc);
+    }
+  }
+  // lanes of one wave per SIMD on the current device (compute units x 4
+  // SIMDs x 64), queried once per device
+  static int64_t pin_lanes() {
+    static std::atomic<int> cache[64];  // compute units + 1 (0: not yet queried)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 65536;
+    int v = dev >= 0 && dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0;
+    if (v == 0) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return 65536;
+      v = cus + 1;
+      if (dev >= 0 && dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return (int64_t)(v - 1) * 4 * 64;
   }
 };
 

@@ -379,11 +379,58 @@ def group_order() -> tuple:
     return order
 
 
-def motion_groups(motion):
+def motion_groups(motion, resident_waves: int | None = None):
     """Grouping for qt_rollout_grouped: (order int32 [n], seg_motion, seg_end).
     A device tensor of motion types is grouped on the device (stable sort, one
     5-element read back); a numpy array on the host.  Groups follow
-    group_order(); within a group, episodes keep their index order."""
+    group_order(); within a group, episodes keep their index order.
+
+    resident_waves (the waves the grouped kernel holds at once on the device:
+    2 per SIMD): a batch of at most that many waves runs as one resident set,
+    its first half of the waves the first on their SIMDs and the second half
+    beside them; the group straddling the middle is then split at it and its
+    second part moved to the end (pair_rounds), so that the second half opens
+    with the short groups instead of the rest of a long one (config 5's 8-GPU
+    shard, 2,048 waves: 2.91-2.95 -> 2.85-2.86 ms, profiles/r06/order_ab.jsonl)."""
+    order, kinds, ends = _motion_groups(motion)
+    if resident_waves:
+        order, kinds, ends = pair_rounds(order, kinds, ends, resident_waves)
+    return order, kinds, ends
+
+
+def pair_rounds(order, kinds, ends, resident_waves: int):
+    """motion_groups' layout for a batch that fits one resident set: the
+    group holding the middle wave (grouped_waves' layout, riders included)
+    split there at a wave boundary and its second part moved to the end
+    (<= 8 segments, each a whole motion; the stationary group is not split,
+    its riders keep filling the other groups' last waves)."""
+    total = grouped_waves(kinds, ends)
+    if total > resident_waves or len(kinds) >= 8 or total < 4:
+        return order, kinds, ends
+    half, w, start = total // 2, 0, 0
+    for i, (k, e) in enumerate(zip(kinds, ends)):
+        cnt = e - start
+        own = (cnt + 63) // 64
+        if w + own > half:
+            if k == 0 or w == half:
+                return order, kinds, ends
+            cut = start + (half - w) * 64  # whole waves of this group before the middle
+            if cut <= start or cut >= e:
+                return order, kinds, ends
+            if isinstance(order, torch.Tensor):
+                new = torch.cat([order[:cut], order[e:], order[cut:e]])
+            else:
+                new = np.concatenate([order[:cut], order[e:], order[cut:e]])
+            counts = [b - a for a, b in zip([0] + list(ends[:-1]), ends)]
+            seq = list(zip(kinds[:i], counts[:i])) + [(k, cut - start)] + list(zip(kinds[i + 1:], counts[i + 1:])) \
+                + [(k, e - cut)]
+            return new, [m for m, _ in seq], [int(v) for v in np.cumsum([c for _, c in seq])]
+        w += own
+        start = e
+    return order, kinds, ends
+
+
+def _motion_groups(motion):
     GROUP_ORDER = group_order()
     pos = np.empty(5, np.int64)
     pos[list(GROUP_ORDER)] = np.arange(5)
@@ -397,6 +444,15 @@ def motion_groups(motion):
         counts = np.bincount(m, minlength=5)  # motion types 0..4: O(n), no sort
     kinds = [k for k in GROUP_ORDER if counts[k]]
     return order, kinds, [int(v) for v in np.cumsum(counts[kinds])]
+
+
+def resident_grouped_waves(device) -> int | None:
+    """Waves the grouped kernel holds at once on `device`: 2 per SIMD
+    (QT_GROUPED_WAVES), 4 SIMDs per compute unit.  None (no round pairing in
+    motion_groups) with QT_PAIR_ROUNDS=0, an A/B knob."""
+    if os.environ.get("QT_PAIR_ROUNDS") == "0":
+        return None
+    return torch.cuda.get_device_properties(device).multi_processor_count * 4 * 2
 
 
 def riders_on() -> bool:
@@ -419,6 +475,8 @@ def grouped_waves(seg_motion, seg_end, riders: bool | None = None) -> int:
             cnt.append([int(m), int(e - prev), 0])  # motion, own episodes, riders
         prev = e
     stat = next((i for i, c in enumerate(cnt) if c[0] == 0), None)
+    if len(cnt) > 8:  # more groups than the one-launch form takes: one launch set per group, no riders
+        riders = False
     if riders and stat is not None:
         avail = cnt[stat][1]
         for i, c in enumerate(cnt):

@@ -236,7 +236,8 @@ def build_batch(controller: BatchedRiccatiLQR, env_config, n: int, seeds=None, m
     mo = None if kinds is None else torch.as_tensor(kinds, device=dev)
     groups = None
     if kinds is not None and order is None and group_motion and kinds.size and np.any(kinds != kinds.flat[0]):
-        order, seg_motion, seg_end = core.motion_groups(mo)  # on the device: the order stays there
+        # on the device: the order stays there; a batch of one resident set pairs its rounds
+        order, seg_motion, seg_end = core.motion_groups(mo, core.resident_grouped_waves(dev))
         groups = (seg_motion, seg_end)
     if plant_mass is None:
         pm = None

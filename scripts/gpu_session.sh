@@ -21,6 +21,8 @@
 #              with stationary riders and without (QT_RIDERS=0), alternating ALT times; then the
 #              whole config both ways
 #   small      the fused rollout at small per-GPU batches (scripts/small_batch.py), with a kernel trace
+#   pairing    config 5's 8-GPU shards with the resident set's rounds paired and without
+#              (QT_PAIR_ROUNDS=0), alternating ALT times over RANKS
 #   shards     the per-rank shards of configs 4 and 5 for W = 1, 2, 4, 8 ranks (first and last rank),
 #              timed on one GPU (run_workload.py --shard): the predicted 1/2/4/8-GPU table
 set -o pipefail
@@ -65,6 +67,11 @@ for step in ${STEPS:-tests smoke bench}; do
              python3 scripts/small_batch.py --reps 10 > $O/small_trace.log 2>&1 || fail small $O/small_trace.log
            cp $(find $O/small_trace -name "*kernel_stats.csv" | head -1) $O/small_kernel_stats.csv
            cp $(find $O/small_trace -name "*kernel_trace.csv" | head -1) $O/small_kernel_trace.csv ;;
+    pairing) for a in $(seq 1 ${ALT:-1}); do for r in ${RANKS:-0 1 2 3 4 5 6 7}; do for pr in 1 0; do
+               QT_PAIR_ROUNDS=$pr timeout -k 10 120 python -u scripts/run_workload.py --config 5 --shard $r/8 --repeat 10 \
+                 | sed "s/^/{\"pair_rounds\": $pr, \"r\": /; s/$/}/" >> $O/pairing.jsonl 2>> $O/pairing.err \
+                 || fail pairing $O/pairing.err
+             done; done; done ;;
     shards) for c in 4 5; do for w in 1 2 4 8; do for r in $(echo 0 $((w - 1)) | tr ' ' '\n' | sort -u); do
               timeout -k 10 200 python -u scripts/run_workload.py --config $c --shard $r/$w --repeat 10 \
                 >> $O/shards.jsonl 2>> $O/shards.err || fail shards $O/shards.err

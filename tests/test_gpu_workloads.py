@@ -226,6 +226,7 @@ def test_riders_bitwise_and_deferred(qt, monkeypatch):
     n = 1100  # 220 per motion: each group's last wave has 36 free lanes
     motion = [i % 5 for i in range(n)]
     ctl = BatchedRiccatiLQR({"dt": 0.01})
+    monkeypatch.setenv("QT_PAIR_ROUNDS", "0")  # the plain group layout: the slots named below
     runs = {}
     for riders in ("1", "0"):
         monkeypatch.setenv("QT_RIDERS", riders)

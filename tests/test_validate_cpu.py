@@ -94,6 +94,44 @@ def test_grouped_waves_with_stationary_riders(monkeypatch):
     assert core.grouped_waves(*core.motion_groups(workloads.motion_of(0, 131072))[1:]) == 2050
 
 
+def test_pair_rounds_layout():
+    """core.motion_groups with resident_waves (core.pair_rounds): a batch of
+    one resident set has the group holding its middle wave split there at a
+    wave boundary, the second part moved to the end; every segment is one
+    motion, the order a permutation, the wave count unchanged; a batch beyond
+    one resident set, or whose middle falls on a group boundary or in the
+    stationary group, keeps the plain layout."""
+    import numpy as np
+
+    from quadtrack import workloads
+
+    for lo, hi, split in ((0, 131072, True), (917504, 1048576, True), (0, 1048576, False), (0, 1100, True),
+                          (777777, 778477, False), (0, 64, False)):
+        m = workloads.motion_of(lo, hi)
+        order, sm, se = core.motion_groups(m, 2048)
+        po, psm, pse = core.motion_groups(m)
+        assert sorted(order.tolist()) == list(range(hi - lo))
+        start = 0
+        for k, e in zip(sm, se):
+            assert np.all(m[order[start:e]] == k)
+            start = e
+        assert core.grouped_waves(sm, se) == core.grouped_waves(psm, pse)
+        assert (len(sm) == len(psm) + 1) == split, (lo, hi, sm)
+        if split:
+            assert sm[-1] == sm[len(psm) // 2] and sm[:len(psm)] == psm  # [3, 4, 2, 1, 0] + [2]
+            half = core.grouped_waves(psm, pse) // 2
+            first = sum(-(-(b - a) // 64) for a, b in zip([0] + se[:len(psm) // 2], se[:len(psm) // 2 + 1]))
+            assert first == half
+    counts = [5000, 0, 0, 300, 0]  # the middle in the stationary group, which is never split
+    m = np.concatenate([np.full(c, k, np.int8) for k, c in enumerate(counts)])
+    order, sm, se = core.motion_groups(m, 2048)
+    assert sm == [3, 0]
+    counts = [300, 0, 0, 5000, 0]  # the middle inside the long group: its second part after the stationary one
+    m = np.concatenate([np.full(c, k, np.int8) for k, c in enumerate(counts)])
+    order, sm, se = core.motion_groups(m, 2048)
+    assert sm == [3, 0, 3] and se[0] == 41 * 64
+
+
 def test_group_order_knob_is_validated_when_used(monkeypatch):
     """QT_GROUP_ORDER (an A/B knob) is read when a grouping is made: a
     malformed value raises there with the variable named, and never breaks
