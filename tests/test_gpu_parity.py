@@ -504,7 +504,8 @@ def test_mixed_motion_order_permutation(qt):
     assert b.groups is None
     r = run_closed_loop(ctl, {}, n=n, batch=b, max_steps=500)
     g = run_closed_loop(ctl, {}, n=n, seeds=np.arange(n), motion=motion, max_steps=500)
-    assert g.batch.groups is not None and list(g.batch.groups[0]) == list(core.group_order())
+    # group order (a batch of one resident set has its middle group split, core.pair_rounds)
+    assert g.batch.groups is not None and list(g.batch.groups[0])[:5] == list(core.group_order())
     assert torch.equal(a.metrics, r.metrics)
     assert torch.equal(a.state.x, r.state.x)
     np.testing.assert_allclose(a.metrics.cpu().numpy(), g.metrics.cpu().numpy(), rtol=1e-9, atol=1e-9)
