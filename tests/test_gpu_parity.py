@@ -482,6 +482,26 @@ def test_deferred_waves_run_exact_pass(qt):
     np.testing.assert_allclose(xf, xe, rtol=1e-9, atol=1e-9)
 
 
+def test_exact_pinned_and_unpinned_bitwise(qt):
+    """The exact kernel's two instantiations (ExactLaunch: uniforms pinned in
+    VGPRs while the launch holds at most one wave per SIMD, the two-wave
+    unpinned form above) compute the same numbers: the first 640 episodes of
+    a 70,016-episode recorded run (unpinned) equal a 640-episode run
+    (pinned) bit for bit, records included."""
+    from quadtrack.controllers import BatchedRiccatiLQR
+    from quadtrack.rollout import run_closed_loop
+
+    ctl = BatchedRiccatiLQR({"dt": 0.01, "use_lqi": True, "q_int": [1e-3, 1e-3, 1e-2]})
+    cfg = {"target": {"motion_type": "sinusoidal"}}
+    m, big = 640, 70016
+    assert big > torch.cuda.get_device_properties(0).multi_processor_count * 4 * 64
+    a = run_closed_loop(ctl, cfg, n=big, seeds=np.arange(big), max_steps=40, record=True)
+    b = run_closed_loop(ctl, cfg, n=m, seeds=np.arange(m), max_steps=40, record=True)
+    assert torch.equal(a.metrics[:, :m], b.metrics)
+    assert torch.equal(a.state.x[:, :m], b.state.x)
+    assert torch.equal(a.record[:, :, :m], b.record)
+
+
 def test_mixed_motion_order_permutation(qt):
     """Mixed motion types: the per-step runtime-motion kernel, the same kernel
     under a permuting `order`, and the grouped motion-specialised launches
