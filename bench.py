@@ -441,13 +441,14 @@ def step_api_leg(args, cfg, dev):
     ms = e0.elapsed_time(e1) / k
     # what the timed loop computed: the first 1,024 episodes' state after its
     # 10 + k steps against the fused rollout of the same episodes for as many
-    # steps (another kernel: the closed-form fast step, not the staged exact
-    # step the per-step API runs)
+    # steps (another kernel: the fused loop's closed-form exact step, with
+    # recording so that it is not the bench kernel, whose profile averages
+    # over its dispatches)
     from quadtrack.rollout import run_closed_loop
 
     m = min(n, 1024)
     ref = run_closed_loop(BatchedRiccatiLQR({"dt": 0.01}, device=dev), cfg, n=m, seeds=np.arange(m),
-                          max_steps=10 + k)
+                          max_steps=10 + k, record=True)
     got = env.frame.f[0:12, :m]
     check = float((got - ref.state.x).abs().max().item())
     gbps = STEP_API_BYTES * n / (ms * 1e-3) / 1e9
