@@ -54,7 +54,7 @@ KERNEL_TAG = "rollout_kernel<2, 1, 6, false, true"
 # The committed rocprofv3 session this line reads its profile, traffic and
 # issued-FP64 numbers from (scripts/profile_session.sh's condensed CSVs):
 # one named directory, never "the newest".  --profile-dir overrides it.
-PROFILE_DIR = "profiles/r05"
+PROFILE_DIR = "profiles/r06"
 # Warm-up floor: a fresh box's first ~0.5 s of passes run at lower clocks
 # (round 2: --warmup 5, 8 ms of GPU work, measured ~7% below --warmup 20), so
 # the warm-up runs for at least this long whatever --warmup says.
