@@ -310,11 +310,12 @@ __device__ __forceinline__ void run_steps(const qt_env_params& e0, const qt_ctrl
                                           const Gains<KC, KS>& G0, const FFLane& fl, double* x, double* integ,
                                           Target& tg, double& t, Acc& a, int nsteps, double* __restrict__ rec,
                                           int64_t n, int64_t ep, double* __restrict__ reward = nullptr) {
-  // the exact step: its loop-invariant uniforms (env limits, controller
-  // clamps, gains, plant) held in VGPRs (vpin) instead of spilled SGPRs
-  // PIN (the exact kernel's launch choice, ExactLaunch): off for batches of
-  // more than one wave per SIMD, where a second resident wave (unpinned: <=
-  // 256 VGPRs) hides the FP64 latency that pinning's fewer instructions cannot
+  // The exact step holds its loop-invariant uniforms (env limits and centre,
+  // controller clamps, plant; QT_EXACT_VPIN) and its Taylor coefficients in
+  // VGPRs (vpin, SmallCoef::pin) instead of spilled SGPRs.  PIN (the exact
+  // kernel's launch choice, ExactLaunch) turns that off for batches of more
+  // than one wave per SIMD, where a second resident wave (unpinned: <= 256
+  // VGPRs) hides the FP64 latency that pinning's fewer instructions cannot.
   constexpr int kPinBits = FAST ? QT_FAST_VPIN : (PIN ? QT_EXACT_VPIN : 0);
   constexpr bool kPin = kPinBits & 1;
   constexpr bool kPinLin = kPinBits & 2;
