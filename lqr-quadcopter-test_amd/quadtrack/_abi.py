@@ -196,6 +196,38 @@ def raw_stream(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
 
+try:  # the current device's ordinal without torch.cuda.current_device()'s lazy-init checks
+    _get_device = torch._C._cuda_getDevice
+except AttributeError:  # pragma: no cover
+    _get_device = None
+
+
+class _Current:
+    """A no-op context: the launch's device is already the current one."""
+
+    __slots__ = ()
+
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_CURRENT = _Current()
+
+
+def on_device(dev: torch.device):
+    """`torch.cuda.device(dev)`, or a no-op context when dev is already the
+    current device: the per-step API enters it once per launch, and entering
+    and leaving torch's context costs ~1.5 us of host time per step
+    (profiles/r06/step_host_parts.jsonl), more than the kernel of a
+    65,536-episode step takes on the GPU."""
+    if _get_device is not None and dev.index is not None and _get_device() == dev.index:
+        return _CURRENT
+    return torch.cuda.device(dev)
+
+
 def check(rc: int, what: str):
     if rc != 0:
         raise QuadtrackError(f"{what} failed with status {rc} ({'invalid argument' if rc == -1 else 'HIP launch error'})")

@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from .. import _abi, core
-from .._abi import FB_DONE, FR_X, MOTIONS, check, raw_stream
+from .._abi import FB_DONE, FR_X, MOTIONS, check, on_device, raw_stream
 from ..step import Frame, FramePool, action_tensor
 from . import seeding
 from .config import as_env_config
@@ -159,7 +159,7 @@ class BatchedQuadcopterEnv:
         n, dev = self.num_envs, self.device
         a = action_tensor(actions, n, dev)
         out = self._next_frame()
-        with torch.cuda.device(dev):
+        with on_device(dev):
             check(_abi.load().qt_frame_step(self._env_ref, self._batch_ref, fr.ptr,
                                             _abi.View(a.data_ptr(), a.stride(1), a.stride(0)), out.ptr,
                                             int(self.freeze_done), raw_stream(dev)), "qt_frame_step")
@@ -180,10 +180,10 @@ class BatchedQuadcopterEnv:
         cb = self._closed_batch(controller)
         integ = controller._state_for(n)
         out = self._next_frame()
-        with torch.cuda.device(dev):
+        with on_device(dev):
             check(_abi.load().qt_frame_closed_step(
                 self._env_ref, controller._ctrl_ref, cb, fr.ptr, None if integ is None else integ.data_ptr(),
-                out.ptr, out.act.data_ptr(), int(self.freeze_done), raw_stream(dev)), "qt_frame_closed_step")
+                out.ptr, out.act_ptr, int(self.freeze_done), raw_stream(dev)), "qt_frame_closed_step")
         self._frame = out.seal()
         return out.step_result(with_action=True)
 

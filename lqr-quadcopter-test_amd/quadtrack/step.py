@@ -34,7 +34,8 @@ import numpy as np
 import torch
 
 from . import _abi
-from ._abi import (FB_DONE, FB_ROWS, FB_TERM, FC_ROWS, FR_ROWS, FR_TIME, Batch, ObsView, View, check, raw_stream)
+from ._abi import (FB_DONE, FB_ROWS, FB_TERM, FC_ROWS, FR_ROWS, FR_TIME, Batch, ObsView, View, check, on_device,
+                   raw_stream)
 
 F64 = torch.float64
 
@@ -64,6 +65,14 @@ def _storage_uses(t: torch.Tensor) -> int:
     return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
 
 
+def _stor_uses(stor) -> int:
+    """_storage_uses of a storage object the caller keeps (Frame._stor: the
+    count then includes that object, not a temporary)."""
+    if not _CAN_RECYCLE:
+        return 0
+    return torch._C._storage_Use_Count(stor._cdata)
+
+
 class Frame:
     """One step's observation + info block (qt_frame_row): f [25, n] float64,
     c [3, n] int64, b [5, n] int8 views of one device allocation, followed
@@ -87,8 +96,8 @@ class Frame:
     view: 65,536 episodes x 3,000 steps of held views would pin ~51 GB where
     clones take ~1.5 GB."""
 
-    __slots__ = ("n", "buf", "f", "c", "b", "act", "ptr", "version", "_q", "_obs_view", "_views", "_refs",
-                 "_uses", "_info")
+    __slots__ = ("n", "buf", "f", "c", "b", "act", "ptr", "act_ptr", "version", "_q", "_obs_view", "_views",
+                 "_refs", "_uses", "_info", "_stor")
 
     def __init__(self, n: int, device):
         self.n = n
@@ -100,6 +109,9 @@ class Frame:
         self.b = b.view(torch.int8)[:FB_ROWS * n].view(FB_ROWS, n)
         self.act = a.view(4, n)
         self.ptr = self.buf.data_ptr()
+        self.act_ptr = self.act.data_ptr()
+        # the buffer's storage object, held for its use count (_stor_uses)
+        self._stor = self.buf.untyped_storage() if _CAN_RECYCLE else None
         self.version = None  # buf._version once a kernel has written it (seal)
         self._q = None
         self._obs_view = None
@@ -150,16 +162,16 @@ class Frame:
         self._views = (rew, done, self.act.T) + q + tuple(v for _, v in self._info)
 
     def _counts(self):
-        return [sys.getrefcount(v) for v in self._views]
+        return list(map(sys.getrefcount, self._views))
 
     def _snapshot(self):
         # what the frame itself holds (called with no other reference alive)
         self._refs = self._counts()
-        self._uses = _storage_uses(self.buf)
+        self._uses = _stor_uses(self._stor)
 
     def recyclable(self) -> bool:
         """True when no view of this frame is held outside it (see the class doc)."""
-        return (self._views is not None and _CAN_RECYCLE and _storage_uses(self.buf) == self._uses
+        return (self._views is not None and _CAN_RECYCLE and _stor_uses(self._stor) == self._uses
                 and self._counts() == self._refs)
 
     def step_result(self, with_action: bool = False):
@@ -368,7 +380,7 @@ class BatchedControlMixin:
             v, keep = obs_view_of(obs, n, self.device, self.k_cols == 3)
         integ = self._state_for(n)
         out = self._action_out(n)
-        with torch.cuda.device(self.device):  # the launch's stream and pointers are this device's
+        with on_device(self.device):  # the launch's stream and pointers are this device's
             check(_abi.load().qt_compute_action_obs(self._ctrl_ref, self._cb_ref, C.byref(v),
                                                     None if integ is None else integ.data_ptr(), out.buf.data_ptr(),
                                                     None, raw_stream(self.device)), "qt_compute_action_obs")
