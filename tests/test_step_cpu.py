@@ -183,3 +183,34 @@ def test_dlpack_export_keeps_the_frame():
     assert not fr.recyclable()
     del arr
     assert fr.recyclable()
+
+
+def test_on_device_enters_torch_context_only_for_another_device(monkeypatch):
+    """_abi.on_device: a no-op context when the launch's device is the current
+    one (the per-step hot path), torch.cuda.device otherwise (a
+    controller or env on another GPU than the current one)."""
+    monkeypatch.setattr(_abi, "_get_device", lambda: 1)
+    ctx = _abi.on_device(torch.device("cuda", 1))
+    assert ctx is _abi._CURRENT
+    with ctx as v:  # enters and leaves without touching the device
+        assert v is None
+    other = _abi.on_device(torch.device("cuda", 0))
+    assert isinstance(other, torch.cuda.device) and other.idx == 0
+    # no ordinal query available: always torch's context
+    monkeypatch.setattr(_abi, "_get_device", None)
+    assert isinstance(_abi.on_device(torch.device("cuda", 1)), torch.cuda.device)
+
+
+def test_frame_keeps_its_command_pointer_and_storage():
+    """Frame.act_ptr is the command rows' address (after the frame words) and
+    the kept storage object serves the recycling test."""
+    fr = Frame(64, "cpu")
+    assert fr.act_ptr == fr.act.data_ptr() == fr.ptr + frame_words(64) * 8
+    obs = fr.observation()
+    assert not fr.recyclable()  # the observation is held
+    del obs
+    assert fr.recyclable()
+    view = fr.f[0, :8]  # a derived view shares the storage: not recyclable
+    assert not fr.recyclable()
+    del view
+    assert fr.recyclable()
