@@ -56,18 +56,11 @@ class Observation(dict):
 _CAN_RECYCLE = hasattr(torch._C, "_storage_Use_Count")
 
 
-def _storage_uses(t: torch.Tensor) -> int:
-    """Tensors (views included) sharing t's storage, +1 for the temporary;
-    0 on a torch build without the (private) use count, whose frames and
-    action buffers are then never recycled (_CAN_RECYCLE)."""
-    if not _CAN_RECYCLE:
-        return 0
-    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
-
-
 def _stor_uses(stor) -> int:
-    """_storage_uses of a storage object the caller keeps (Frame._stor: the
-    count then includes that object, not a temporary)."""
+    """Tensors (views included) sharing the storage `stor` — an object the
+    caller keeps for this count (Frame._stor, _Out._stor), so it includes
+    that object; 0 on a torch build without the (private) use count, whose
+    frames and action buffers are then never recycled (_CAN_RECYCLE)."""
     if not _CAN_RECYCLE:
         return 0
     return torch._C._storage_Use_Count(stor._cdata)
@@ -250,16 +243,17 @@ class _Out:
     reusable once released (no reference to the view, no other tensor on
     the storage), as Frame.recyclable."""
 
-    __slots__ = ("buf", "view", "_ref", "_uses")
+    __slots__ = ("buf", "view", "_ref", "_uses", "_stor")
 
     def __init__(self, rows: int, n: int, device):
         self.buf = torch.empty(rows, n, dtype=F64, device=device)
         self.view = self.buf.T
+        self._stor = self.buf.untyped_storage() if _CAN_RECYCLE else None  # as Frame._stor
         self._ref = sys.getrefcount(self.view)
-        self._uses = _storage_uses(self.buf)
+        self._uses = _stor_uses(self._stor)
 
     def free(self) -> bool:
-        return _CAN_RECYCLE and sys.getrefcount(self.view) == self._ref and _storage_uses(self.buf) == self._uses
+        return _CAN_RECYCLE and sys.getrefcount(self.view) == self._ref and _stor_uses(self._stor) == self._uses
 
 
 def tensor_view(t: torch.Tensor, rows: int, n: int, name: str, device) -> View:
