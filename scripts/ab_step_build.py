@@ -8,6 +8,8 @@ GPU side is scripts/ab_step.sh):
   cf    env_step_into with the fused exact step's closed-form RK4 (integrate_closed) for states of
         moderate magnitude, the staged RK4 otherwise (180 VGPRs: 2 waves per SIMD)
   cfw3  cf capped at 3 waves per SIMD
+  early the frame rows that depend on time only (target observation, time, step count) computed
+        and stored before the integration, so their stores drain while the step computes (round 6)
 
 Each variant recompiles qt_step.hip only and links it with the in-tree objects of the other
 translation units."""
@@ -40,6 +42,43 @@ CLOSED_FORM_NEW = """  const bool viol = parse_action(e, u, ua);
 """
 
 
+EARLY_OLD = """  double ua[4];
+  const bool viol = parse_action(e, u, ua);
+  integrate(e, pl, x, ua);
+  t += e.dt;
+  // np.clip's NaN propagation kept: a caller's action may drive the state anywhere
+  const int term = constrain_terminate<true>(e, x, t);
+  Target tg;
+  target_state<true>(e, motion, pt, t, tg);
+"""
+EARLY_NEW = """  double ua[4];
+  t += e.dt;
+  Target tg;
+  target_state<true>(e, motion, pt, t, tg);
+  store_target(O, n, ep, tg);
+  O.f[QT_FR_TIME * n + ep] = t;
+  O.c[QT_FC_STEP * n + ep] = k.step + 1;
+  const bool viol = parse_action(e, u, ua);
+  integrate(e, pl, x, ua);
+  // np.clip's NaN propagation kept: a caller's action may drive the state anywhere
+  const int term = constrain_terminate<true>(e, x, t);
+"""
+EARLY_STORES_OLD = """  store_target(O, n, ep, tg);
+  O.f[QT_FR_TIME * n + ep] = t;
+  O.f[QT_FR_ERR * n + ep] = err;"""
+EARLY_STORES_NEW = """  O.f[QT_FR_ERR * n + ep] = err;"""
+EARLY_STEP_OLD = """  O.c[QT_FC_STEP * n + ep] = k.step;
+  O.c[QT_FC_VIOLATIONS"""
+EARLY_STEP_NEW = """  O.c[QT_FC_VIOLATIONS"""
+
+
+def early(src):
+    for a, b in ((EARLY_OLD, EARLY_NEW), (EARLY_STORES_OLD, EARLY_STORES_NEW), (EARLY_STEP_OLD, EARLY_STEP_NEW)):
+        assert src.count(a) == 1, a
+        src = src.replace(a, b)
+    return src
+
+
 def waves(src, w):
     return src.replace(KERNEL, KERNEL.replace("__global__ __launch_bounds__(kBlock)",
                                               f"__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu({w})))"))
@@ -49,7 +88,7 @@ def main():
     head = open(os.path.join(PKG, "csrc", "qt_step.hip")).read()
     assert CLOSED_FORM_OLD in head and KERNEL in head
     cf = head.replace(CLOSED_FORM_OLD, CLOSED_FORM_NEW)
-    variants = {"head": head, "w4": waves(head, 4), "cf": cf, "cfw3": waves(cf, 3)}
+    variants = {"head": head, "w4": waves(head, 4), "cf": cf, "cfw3": waves(cf, 3), "early": early(head)}
     objs = [os.path.join(PKG, "build", f) for f in ("qt_dare.o", "qt_rollout.o", "qt_rollout_fast.o", "qt_seed.o")]
     for name, src in variants.items():
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
