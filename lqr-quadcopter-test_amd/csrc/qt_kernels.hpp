@@ -1233,6 +1233,12 @@ void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, i
                  const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr, const BatchDev& b,
                  const qt_state& st, int nsteps, const LaunchConst& lc);
 
+// The pair-lane yaw-at-rest flavour (qt_pair.hpp; qt_rollout_fast.hip): one
+// episode on two lanes, for a batch of at most one wave per SIMD in pairs;
+// motion QT_MOTION_LINEAR or QT_MOTION_STATIONARY, grid of 2 n lanes.
+void launch_pair(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                 const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, const LaunchConst& lc);
+
 // Calls L::template run<MOTION, KC, FF, KS>(args...) for a runtime (kc, ff, ks, motion);
 // PID (kc 3) never commands yaw and always takes the structured form.
 template <class L, int KC, bool FF, bool KS, class... A>

@@ -644,6 +644,25 @@ int dual_below() {
   return (int)x;
 }
 
+// The pair-lane yaw-at-rest flavour (qt_pair.hpp): on unless QT_PAIR=0 (an
+// A/B and test knob, read at each launch).
+bool pair_on() {
+  const char* s = getenv("QT_PAIR");
+  return !(s && s[0] == '0' && s[1] == '\0');
+}
+
+// A yaw-at-rest launch the pair flavour covers: one structured 6-column gain,
+// no feed-forward, no per-episode plant or hover thrust, a linear or
+// stationary target for every episode, no rewards, the slots in episode order,
+// and at most one wave per SIMD in pairs (2 n lanes; beyond that the pairs'
+// 173 instructions per step on two waves per SIMD lose to one wave of 230:
+// profiles/r06/split_step.jsonl).
+bool pair_fits(int kc, bool ff, bool ks, bool grouped, int motion, const BatchDev& b, const LaunchConst& lc) {
+  return pair_on() && !grouped && kc == 6 && ks && !ff && !b.plant_mass && !b.hover && !b.k_per_episode &&
+         !lc.reward && (motion == QT_MOTION_LINEAR || motion == QT_MOTION_STATIONARY) && b.nseg == 0 && !b.order &&
+         b.seg_check < 0 && b.slot0 == 0 && b.slot_end == b.n && b.n > 0 && 2 * b.n <= ExactLaunch::pin_lanes();
+}
+
 // The step flavour a launch can take (launch-level preconditions).
 int flavor_for(int kc, bool ks, bool no_yaw, const qt_env_params& e, const qt_ctrl_params& c, const double* rec) {
   const bool fast = QT_ABLATE == 0 && rec == nullptr && fast_path_ok(e, c);
@@ -717,7 +736,10 @@ int launch_rollout(int kc, bool ff, bool ks, bool no_yaw, int motion, int grid, 
   if (flavor != kExact) {
     lc.defer_flag = defer_flag_for(s);  // null (no flag: the exact pass tests every wave) if unavailable
     lc.epoch = g_defer_epoch.fetch_add(1, std::memory_order_relaxed) + 1;
-    launch_fast(flavor, uni, grouped, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
+    if (flavor == kYaw0 && pair_fits(kc, ff, ks, grouped, motion, b, lc))
+      launch_pair(motion, (int)((2 * b.n + kBlock - 1) / kBlock), s, e, c, cr, b, st, nsteps, lc);
+    else
+      launch_fast(flavor, uni, grouped, kc, ff, ks_eff, motion, grid, s, e, c, cr, b, st, nsteps, lc);
     if (hipGetLastError() != hipSuccess) return QT_ELAUNCH;
     lc.fresh_off = nullptr;  // the fast kernel stored the reset state of the waves it left
   }

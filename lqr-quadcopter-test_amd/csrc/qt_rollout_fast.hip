@@ -23,6 +23,7 @@ __device__ unsigned long long g_qt_stamps[kStampWaves][6];  // memtime x2, realt
 #endif
 
 #include "qt_kernels.hpp"
+#include "qt_pair.hpp"
 
 namespace qtk {
 
@@ -59,6 +60,14 @@ void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, i
     dispatch_rollout<GroupedLaunch>(kc, ff, ks, -1, grid, s, e, c, cr, b, st, nsteps, lc);
   else
     dispatch_rollout<FastLaunch>(kc, ff, ks, motion, flavor, uni, grid, s, e, c, cr, b, st, nsteps, lc);
+}
+
+void launch_pair(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                 const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, const LaunchConst& lc) {
+  if (motion == QT_MOTION_LINEAR)
+    rollout_pair_kernel<QT_MOTION_LINEAR><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
+  else
+    rollout_pair_kernel<QT_MOTION_STATIONARY><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
 }
 
 }  // namespace qtk
