@@ -26,9 +26,10 @@
 // (tests/test_gpu_workloads.py::test_pair_flavour_bitwise_*).
 //
 // Scope (launch_rollout checks it on the host): the yaw-at-rest flavour with
-// a structured 6-column LQR gain shared by the batch, no feed-forward, no
-// per-episode mass or hover thrust, a linear or stationary target for the
-// whole batch, no rewards, no motion groups; QT_PAIR=0 turns it off.
+// structured 6-column LQR gains (shared, or per episode: the tuner's
+// candidates), no feed-forward, no per-episode mass or hover thrust, one
+// target motion for the whole batch (periodic targets carry their rotor in
+// both lanes), no rewards, no motion groups; QT_PAIR=0 turns it off.
 #pragma once
 
 #include "qt_kernels.hpp"
@@ -109,7 +110,8 @@ template <int MOTION>
 __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_params& c, const qt_criteria& cr,
                                          const Pattern& pt, double hover, const Gains<6, true>& G, int a, double* x,
                                          Target& tg, double& t, Acc& acc_out, int nsteps, const LaunchConst& k) {
-  static_assert(MOTION == QT_MOTION_LINEAR || MOTION == QT_MOTION_STATIONARY, "pair flavour: a fixed-direction target");
+  // periodic targets carry their rotor (run_yaw0's kRotor; no feed-forward)
+  constexpr bool kRotor = MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_FIGURE8;
   constexpr int kNeg = -(1 << 30);
   // The loop's uniforms (closed-form maps, plant, gains, clamps) held in VGPRs
   // (vpin): with them and the launch constants in scalar registers the kernel
@@ -135,7 +137,13 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
   // lane selects as exact 0 / 1 factors where one FP64 slot replaces a select
   const double af = a, nf = 1.0 - af, am1 = af - 1.0;
   // the observation re-derived from t, as run_yaw0 does at launch start
-  target_state<false, true>(e, MOTION, pt, t, tg);
+  double rs[3] = {0.0, 0.0, 0.0}, rc[3] = {1.0, 1.0, 1.0};  // carried target rotor
+  if constexpr (kRotor) {
+    rotor_init<MOTION>(pt, t, rs, rc);
+    target_from_rotor<false, MOTION>(e, pt, rs, rc, tg);
+  } else {
+    target_state<false, true>(e, MOTION, pt, t, tg);
+  }
   // this lane's axis and angle: a = 0 roll and y, a = 1 pitch and x
   const double Kp = a ? G.k[4] : G.k[2], Kv = a ? G.k[5] : G.k[3];
   const double cen_h = a ? e.center[0] : e.center[1], ch = a ? pt.c0 : pt.c1;
@@ -229,8 +237,13 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
       vz = fma(tm, svz, fma(L.cv, vz, L.gv));
       ang = fma(Rl.ay, w, fma(Rl.au, ua, ang));
       w = fma(Rl.wy, w, Rl.wu * ua);
+      const double t0 = t;
       t += dt;
-      if constexpr (MOTION == QT_MOTION_LINEAR) {  // target_state (linear): center + c t
+      if constexpr (kRotor) {  // the rotor turned by one step (rotor_advance), the whole target from it
+        rotor_advance<MOTION>(k, (t - t0) - dt, rs, rc);
+        target_from_rotor<false, MOTION>(e, pt, rs, rc, tg);
+        tph = a ? tg.p[0] : tg.p[1], tvh = a ? tg.v[0] : tg.v[1], tpz = tg.p[2], tvz = tg.v[2];
+      } else if constexpr (MOTION == QT_MOTION_LINEAR) {  // target_state (linear): center + c t
         tph = cen_h + ch * t;
         tpz = cz + pt.c2 * t;
         tvh = ch, tvz = pt.c2;
@@ -326,28 +339,31 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
   gather(xf);
   x[0] = xf[0], x[1] = xf[1], x[2] = xf[2], x[3] = xf[3], x[4] = xf[4], x[5] = xf[5];
   x[6] = xf[6], x[7] = xf[7], x[9] = xf[9], x[10] = xf[10];
-  const double tpp = pair_swap(tph), tvp = pair_swap(tvh);
-  tg.p[0] = a ? tph : tpp, tg.p[1] = a ? tpp : tph, tg.p[2] = tpz;
-  tg.v[0] = a ? tvh : tvp, tg.v[1] = a ? tvp : tvh, tg.v[2] = tvz;
-  tg.a[0] = tg.a[1] = tg.a[2] = 0.0;  // target_state without feed-forward (linear, stationary)
+  if constexpr (!kRotor) {  // (a periodic target's tg is the last step's whole target already)
+    const double tpp = pair_swap(tph), tvp = pair_swap(tvh);
+    tg.p[0] = a ? tph : tpp, tg.p[1] = a ? tpp : tph, tg.p[2] = tpz;
+    tg.v[0] = a ? tvh : tvp, tg.v[1] = a ? tvp : tvh, tg.v[2] = tvz;
+    tg.a[0] = tg.a[1] = tg.a[2] = 0.0;  // target_state without feed-forward (linear, stationary)
+  }
 }
 
 // One pair-lane wave per 32 episodes; the deferral test runs over the exact
 // pass's 64-episode waves (both pair waves of one decide alike), so a wave the
-// exact pass skips is one this launch ran whole.
-template <int MOTION>
+// exact pass skips is one this launch ran whole.  PERK: per-episode gains
+// (qt_batch.k_per_episode, the tuner's candidates), else one shared gain.
+template <int MOTION, bool PERK>
 __global__ __launch_bounds__(kBlock) void rollout_pair_kernel(qt_env_params e, qt_ctrl_params c, qt_criteria cr,
                                                               BatchDev b, qt_state st, int nsteps, LaunchConst lc) {
   const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t n = b.n;
   const double hover = c.hover_thrust;
   const Plant& pl = lc.pl;
-  Gains<6, true> G;
-  load_gains<6, true, true>(b, 0, G);
   {
     const int64_t te = ((g >> 7) << 6) + (g & 63);  // this lane's episode of the exact pass's wave
     bool ok = true;
     if (te < n) {
+      Gains<6, true> G;
+      load_gains<6, true, !PERK>(b, te, G);
       const Pattern pt = pattern_of(b, e, MOTION, te);
       double x[12];
       Target tg;
@@ -387,6 +403,8 @@ __global__ __launch_bounds__(kBlock) void rollout_pair_kernel(qt_env_params e, q
   const int64_t ep = g >> 1;
   if (ep >= n) return;  // both lanes of a pair leave together
   const int a = (int)(g & 1);
+  Gains<6, true> G;
+  load_gains<6, true, !PERK>(b, ep, G);
   const Pattern pt = pattern_of(b, e, MOTION, ep);
   double x[12];
   Target tg;
@@ -395,6 +413,13 @@ __global__ __launch_bounds__(kBlock) void rollout_pair_kernel(qt_env_params e, q
   pair_episode_start<MOTION>(e, b, st, lc, ep, pt, x, tg, t, acc);
   run_pair<MOTION>(e, c, cr, pt, hover, G, a, x, tg, t, acc, nsteps, lc);
   if (a) return;
+  if (MOTION == QT_MOTION_CIRCULAR || MOTION == QT_MOTION_SINUSOIDAL || MOTION == QT_MOTION_FIGURE8) {
+    // the stored observation carries the reference's acceleration (rollout_lane)
+    Target full;
+    target_state<true>(e, MOTION, pt, t, full);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tg.a[i] = full.a[i];
+  }
 #pragma unroll
   for (int i = 0; i < 12; ++i) st.x[i * n + ep] = x[i];
   if (lc.fresh_off && st.integ) {  // a fresh pass stores the zeros qt_reset would (rollout_lane)

@@ -651,15 +651,15 @@ bool pair_on() {
   return !(s && s[0] == '0' && s[1] == '\0');
 }
 
-// A yaw-at-rest launch the pair flavour covers: one structured 6-column gain,
-// no feed-forward, no per-episode plant or hover thrust, a linear or
-// stationary target for every episode, no rewards, the slots in episode order,
-// and at most one wave per SIMD in pairs (2 n lanes; beyond that the pairs'
-// 173 instructions per step on two waves per SIMD lose to one wave of 230:
-// profiles/r06/split_step.jsonl).
+// A yaw-at-rest launch the pair flavour covers: structured 6-column gains
+// (shared or per episode), no feed-forward, no per-episode plant or hover
+// thrust, one motion type for every episode, no rewards, the slots in episode
+// order, and at most one wave per SIMD in pairs (2 n lanes; beyond that the
+// pairs' ~170 instructions per step on two waves per SIMD lose to one wave of
+// ~230: profiles/r06/split_step.jsonl).
 bool pair_fits(int kc, bool ff, bool ks, bool grouped, int motion, const BatchDev& b, const LaunchConst& lc) {
-  return pair_on() && !grouped && kc == 6 && ks && !ff && !b.plant_mass && !b.hover && !b.k_per_episode &&
-         !lc.reward && (motion == QT_MOTION_LINEAR || motion == QT_MOTION_STATIONARY) && b.nseg == 0 && !b.order &&
+  return pair_on() && !grouped && kc == 6 && ks && !ff && !b.plant_mass && !b.hover && !lc.reward &&
+         motion >= QT_MOTION_STATIONARY && motion <= QT_MOTION_FIGURE8 && b.nseg == 0 && !b.order &&
          b.seg_check < 0 && b.slot0 == 0 && b.slot_end == b.n && b.n > 0 && 2 * b.n <= ExactLaunch::pin_lanes();
 }
 

@@ -62,12 +62,27 @@ void launch_fast(int flavor, bool uni, bool grouped, int kc, bool ff, bool ks, i
     dispatch_rollout<FastLaunch>(kc, ff, ks, motion, flavor, uni, grid, s, e, c, cr, b, st, nsteps, lc);
 }
 
+namespace {
+template <int MOTION>
+void launch_pair_motion(int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
+                        const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps,
+                        const LaunchConst& lc) {
+  if (b.k_per_episode)
+    rollout_pair_kernel<MOTION, true><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
+  else
+    rollout_pair_kernel<MOTION, false><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
+}
+}  // namespace
+
 void launch_pair(int motion, int grid, hipStream_t s, const qt_env_params& e, const qt_ctrl_params& c,
                  const qt_criteria& cr, const BatchDev& b, const qt_state& st, int nsteps, const LaunchConst& lc) {
-  if (motion == QT_MOTION_LINEAR)
-    rollout_pair_kernel<QT_MOTION_LINEAR><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
-  else
-    rollout_pair_kernel<QT_MOTION_STATIONARY><<<grid, kBlock, 0, s>>>(e, c, cr, b, st, nsteps, lc);
+  switch (motion) {
+    case QT_MOTION_LINEAR: launch_pair_motion<QT_MOTION_LINEAR>(grid, s, e, c, cr, b, st, nsteps, lc); break;
+    case QT_MOTION_CIRCULAR: launch_pair_motion<QT_MOTION_CIRCULAR>(grid, s, e, c, cr, b, st, nsteps, lc); break;
+    case QT_MOTION_SINUSOIDAL: launch_pair_motion<QT_MOTION_SINUSOIDAL>(grid, s, e, c, cr, b, st, nsteps, lc); break;
+    case QT_MOTION_FIGURE8: launch_pair_motion<QT_MOTION_FIGURE8>(grid, s, e, c, cr, b, st, nsteps, lc); break;
+    default: launch_pair_motion<QT_MOTION_STATIONARY>(grid, s, e, c, cr, b, st, nsteps, lc); break;
+  }
 }
 
 }  // namespace qtk
