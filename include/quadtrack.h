@@ -290,9 +290,9 @@ int qt_stream_uniform(uint64_t seed, int64_t first, int64_t n, int32_t k, const 
    receives, for every step s of this call, x after the step at
    rec[((s*16 + j) * n) + e] for j < 12 and the applied controller action at j = 12..15.
    A batch of at most one wave per SIMD in lane pairs (n <= 32,768 on MI355X) with
-   a linear or stationary target and one structured LQR gain runs each episode on
-   two lanes (the pair flavour, csrc/qt_pair.hpp), with the same results bit for
-   bit; QT_PAIR=0 in the environment turns it off. */
+   one target motion and structured LQR gains (shared or per episode) runs each
+   episode on two lanes (the pair flavour, csrc/qt_pair.hpp), with the same
+   results bit for bit; QT_PAIR=0 in the environment turns it off. */
 int qt_rollout(const qt_env_params* env, const qt_ctrl_params* ctrl, const qt_criteria* crit,
                const qt_batch* batch, qt_state st, int32_t nsteps, double* rec, void* stream);
 
