@@ -163,7 +163,8 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
   double acc = a ? A.sum_u : A.sum_e;  // lane 0: sum_e, lane 1: sum_u
   double sum_e2 = A.sum_e2, max_e = A.max_e, os_max = A.os_max;
   bool stepped = false;
-  // the whole state from the pair (horizon, vote, finish): x[0..7]
+  // the episode's positions, velocities, roll / pitch and their rates from the
+  // pair (the horizon, the vote, the finish; x[8] and x[11] stay at rest)
   auto gather = [&](double* xf) {
     const double pp = pair_swap(ph), vp = pair_swap(vh), angp = pair_swap(ang), wp = pair_swap(w);
     xf[0] = a ? ph : pp, xf[1] = a ? pp : ph, xf[2] = pz;
