@@ -23,7 +23,7 @@
 // commute, -s == s * -1, (-w) s == w (-s) inside an fma), and a lane's
 // results do not depend on the other lanes of its wave (run_yaw0), so the
 // pair flavour's results are the one-lane flavour's bit for bit
-// (tests/test_gpu_workloads.py::test_pair_flavour_bitwise_*).
+// (tests/test_gpu_pair.py).
 //
 // Scope (launch_rollout checks it on the host): the yaw-at-rest flavour with
 // structured 6-column LQR gains (shared, or per episode: the tuner's
