@@ -179,8 +179,9 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
     const int s_0 = s;
     int rem = nsteps - s_0 > (1 << 29) ? (1 << 29) : nsteps - s_0;
     RateCoef rk;
-    auto step = [&](auto vote) -> bool {
-      constexpr bool VOTE = decltype(vote)::value;
+    // CLAMP: the tilt clamp in a no-vote step (run_yaw0's DUAL body)
+    auto step = [&](auto vote, auto clamp) -> bool {
+      constexpr bool VOTE = decltype(vote)::value, CLAMP = decltype(clamp)::value;
       rk.pin();
       const double a0 = ang;
       // ---- compute_action (riccati_lqr.py:779-967): thrust from z, this lane's rate from its axis
@@ -278,10 +279,12 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
         tiny_sincos((ang - a0) - d4, &sr, &cr);
         rotate_cm(s3, c3, sr, cr, &s0, &c0);
       }
+      if constexpr (VOTE || CLAMP) {
+        ang = clip_num(ang, -kMaxTilt, kMaxTilt);
+        s0 = clip_num(s0, -sm, sm);
+        c0 = fmax(c0, cmx);
+      }
       if constexpr (!VOTE) return false;
-      ang = clip_num(ang, -kMaxTilt, kMaxTilt);
-      s0 = clip_num(s0, -sm, sm);
-      c0 = fmax(c0, cmx);
       --rem;
       double xf[12];
       gather(xf);
@@ -293,22 +296,43 @@ __device__ __forceinline__ void run_pair(const qt_env_params& e, const qt_ctrl_p
     do {
       double xf[12];
       gather(xf);
-      const int H = yaw0_horizon<true, false>(e, k.hz, L, pl, xf, t, rem);
-      using F = std::false_type;
-      for (int j = 4; j <= H; j += 4) {
-        step(F{});
-        step(F{});
-        step(F{});
-        step(F{});
+      int H = yaw0_horizon<true, false>(e, k.hz, L, pl, xf, t, rem);
+      bool clamp_body = false;  // wave-uniform (H comes from ballots)
+      if constexpr (kRotor) {  // run_yaw0's DUAL (the one-lane fresh pass takes it for periodic LQR loops)
+        if (H < k.hz.dual_below) {
+          const int H2 = yaw0_horizon<false, false>(e, k.hz, L, pl, xf, t, rem);
+          if (H2 > H) H = H2, clamp_body = true;
+        }
       }
-      if (H & 2) {
-        step(F{});
-        step(F{});
+      using F = std::false_type;
+      using T = std::true_type;
+      if (kRotor && clamp_body) {
+        for (int j = 4; j <= H; j += 4) {
+          step(F{}, T{});
+          step(F{}, T{});
+          step(F{}, T{});
+          step(F{}, T{});
+        }
+        if (H & 2) {
+          step(F{}, T{});
+          step(F{}, T{});
+        }
+      } else {
+        for (int j = 4; j <= H; j += 4) {
+          step(F{}, F{});
+          step(F{}, F{});
+          step(F{}, F{});
+          step(F{}, F{});
+        }
+        if (H & 2) {
+          step(F{}, F{});
+          step(F{}, F{});
+        }
       }
       rem -= H;
       const int nv = H > 0 ? 0 : (k.hz.on ? kVotedBurst : (1 << 30));
       bool stop = false;
-      for (int j = 0; j < nv && !stop; ++j) stop = step(std::true_type{});
+      for (int j = 0; j < nv && !stop; ++j) stop = step(T{}, F{});
       if (stop) break;
     } while (true);
     const int ran = (nsteps - s_0 > (1 << 29) ? (1 << 29) : nsteps - s_0) - rem;
